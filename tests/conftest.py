@@ -1,0 +1,39 @@
+"""Shared pytest configuration.
+
+Markers:
+  gpu — needs a real MI355X (run on the GPU box with `pytest -m gpu`).  Everything else runs
+        on CPU in the build container.
+"""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+REFERENCE = Path("/root/reference/DistributionRayTracer")
+SCENES = REFERENCE / "P3D_Scenes"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires an MI355X GPU (HIP)")
+    config.addinivalue_line("markers", "reference: requires the reference checkout at /root/reference")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    from oracle import oracle as O
+
+    O.build()
+    return O
+
+
+def have_reference():
+    return (REFERENCE / "bvh.cpp").exists()
+
+
+needs_reference = pytest.mark.skipif(not have_reference(), reason="reference checkout not present")
