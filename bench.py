@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s + frame ms, synthetic 1M-triangle BVH scene, 512x512x64spp.
+
+BASELINE.json metric: "Mrays/s + frame ms at 512x512x64spp, 1M-tri BVH scene, 1/2/4/8 MI355X".
+Workload: N random triangles (centres U[-1,1]^3, vertices c + U[-h,h]^3,
+h = N^-1/3, numpy default_rng(seed)), a 2-triangle floor, mirror material (Ks .5), one quad
++ one point light, balls_low camera, accel bvh, reference semantics (MAX_DEPTH 4, no glossy).
+
+One step = one frame (renderScene, main.cpp:525-738) of the whole hot path on device-resident
+inputs: every pixel sample, every closest-hit and shadow ray, the per-pixel ordered reduce and,
+for N > 1, the RCCL gather of the tile shards to rank 0 plus their reassembly.  Frames are
+tile-sharded (16x16 tiles, tile t -> rank t mod N), so scaling is STRONG (fixed frame).
+
+Rays = closest-hit + shadow traversals per frame, counted by the kernel in an untimed stats
+frame (identical every frame: the keyed RNG makes the frame deterministic).
+
+Prints ONE JSON line on rank 0.  Launch for N > 1:
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+NODE_BYTES, PRIM_BYTES = 64, 48  # one inner-node record (both child boxes), one primitive record
+CAMERA = dict(eye=(2.1, 1.3, 1.7), at=(0.0, 0.0, 0.0), up=(0.0, 0.0, 1.0), fovy=45.0, hither=0.01)
+FLOOR = np.array([[-4, -4, -1.2, 4, -4, -1.2, 4, 4, -1.2], [-4, -4, -1.2, 4, 4, -1.2, -4, 4, -1.2]], np.float32)
+
+
+def synthetic_triangles(n, seed=1):
+    rng = np.random.default_rng(seed)
+    h = n ** (-1.0 / 3.0)
+    c = rng.uniform(-1.0, 1.0, size=(n, 1, 3))
+    v = c + rng.uniform(-h, h, size=(n, 3, 3))
+    return np.concatenate([v.astype(np.float32).reshape(n, 9), FLOOR])
+
+
+def populate(scene, tris, res, spp):
+    """Same calls for the product scene and the oracle scene (P3F-equivalent content)."""
+    scene.set_camera(CAMERA["eye"], CAMERA["at"], CAMERA["up"], CAMERA["fovy"], CAMERA["hither"], res, res, 0.0, 1.0)
+    scene.set_background((0.078, 0.361, 0.753))
+    scene.set_accel("bvh")
+    scene.set_spp(spp)
+    scene.add_light_quad((4, 3, 2), (1, 1, 1), (4, 2, 2), (3, 3, 2), 16)
+    scene.add_light_point((-3, 1, 5), (1, 1, 1))
+    scene.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), 0.5, 30.0827, 0, 1)
+    scene.add_triangles(tris)
+
+
+def cpu_baseline(tris, res, spp, seed, target_s, threads):
+    """The CPU oracle (C++/OpenMP restatement of the reference, oracle/) timed on this host on a
+    bounded sample: a band of full rows of the SAME frame."""
+    from oracle import oracle as O
+
+    O.build()
+    s = O.Scene.new()
+    populate(s, tris, res, spp)
+    t0 = time.time()
+    s.build()
+    build_s = time.time() - t0
+    mid = res // 2
+    t0 = time.time()
+    _, st = s.render(seed=seed, threads=threads, rows=(mid, mid + 1))
+    per_row = max(time.time() - t0, 1e-3)
+    rows = int(max(1, min(res, target_s / per_row)))
+    y0 = max(0, mid - rows // 2)
+    t0 = time.time()
+    _, st = s.render(seed=seed, threads=threads, rows=(y0, y0 + rows))
+    dt = time.time() - t0
+    rays = st["closest_calls"] + st["shadow_calls"]
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"rows {y0}-{y0 + rows - 1} of the {res}x{res}x{spp}spp frame ({rows * res * spp} samples, "
+                      f"{rays} rays) in {dt:.1f} s; oracle BVH build {build_s:.1f} s",
+            "seconds": round(dt, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tris", type=int, default=1_000_000)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+
+    import distributionraytracer_amd as drt
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def log(*a):
+        if rank == 0:
+            print(*a, file=sys.stderr, flush=True)
+
+    t0 = time.time()
+    tris = synthetic_triangles(args.tris, args.seed)
+    scene = drt.Scene()
+    populate(scene, tris, args.res, args.spp)
+    scene.build()
+    info = scene.info()
+    build_s = time.time() - t0
+    log(f"[bench] scene: {info.n_objects} objects, BVH {info.bvh_nodes} nodes, host build {info.build_ms / 1e3:.2f} s "
+        f"(total setup {build_s:.1f} s)")
+    r = drt.Renderer(local)
+    r.upload(scene)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    shard_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world)
+    stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True)
+    frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
+    if world > 1:
+        _, floats = r.shard_layout(shard_p)
+        shard_buf = torch.empty(floats, dtype=torch.float32, device="cuda")
+        gathered = torch.empty(world * floats, dtype=torch.float32, device="cuda")
+
+    def step(p):
+        if world == 1:
+            r.render_device(p, frame.data_ptr(), sptr)
+        else:
+            r.render_device(p, shard_buf.data_ptr(), sptr)
+            dist.all_gather_into_tensor(gathered, shard_buf)
+            if rank == 0:
+                r.unshard_device(shard_p, gathered.data_ptr(), frame.data_ptr(), sptr)
+
+    # untimed stats frame: rays, node visits and primitive tests of this rank's shard
+    step(stats_p)
+    torch.cuda.synchronize()
+    st = r.stats()
+    keys = ["closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_prims", "shadow_prims",
+            "closest_leaf", "shadow_leaf", "samples"]
+    mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
+    tot = mine.clone()
+    if world > 1:
+        dist.all_reduce(tot)
+    tot = dict(zip(keys, tot.tolist()))
+    mine = dict(zip(keys, mine.tolist()))
+    rays_frame = tot["closest_rays"] + tot["shadow_rays"]
+
+    for _ in range(args.warmup):
+        step(shard_p)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(shard_p)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+
+    path_ms, total_ms = r.frame_times(args.steps)
+    kernel_ms = float(np.mean(path_ms)) if len(path_ms) else float("nan")
+    bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
+        PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    tj = Path(args.traffic_json)
+    if world == 1 and tj.exists():
+        try:
+            tr = json.loads(tj.read_text())
+            if tr.get("workload") == f"tris{args.tris}_res{args.res}_spp{args.spp}":
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    value = rays_frame * args.steps / dt / 1e6
+    out = {
+        "metric": "Mrays/s + frame ms at 512x512x64spp, 1M-tri BVH scene, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded random triangle soup, SURVEY.md §8d)",
+        "config": {"workload": f"synthetic {args.tris} triangles + floor, BVH, {args.res}x{args.res}, "
+                               f"{args.spp} spp, MAX_DEPTH 4, 1 quad + 1 point light",
+                   "tris": args.tris, "res": args.res, "spp": args.spp, "accel": "bvh",
+                   "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "path_kernel<BVH,tri>", "bytes_per_launch": int(bytes_launch),
+                     "kernel_ms": round(kernel_ms, 3)},
+        "rays_per_frame": int(rays_frame),
+        "samples_per_frame": int(tot["samples"]),
+        "msamples_per_s": round(tot["samples"] * args.steps / dt / 1e6, 2),
+        "bytes_per_ray": round(bytes_launch / max(1.0, mine["closest_rays"] + mine["shadow_rays"]), 1),
+        "node_visits_per_ray": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
+                                      tot["shadow_leaf"]) / max(1.0, rays_frame), 2),
+        "setup_s": round(build_s, 2),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        try:
+            out["cpu_baseline"] = cpu_baseline(tris, args.res, args.spp, args.seed, args.cpu_seconds, threads)
+            out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        except Exception as e:  # the baseline is reported, never required
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

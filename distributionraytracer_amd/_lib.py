@@ -1,0 +1,155 @@
+"""ctypes bindings for libdrt.so (include/drt.h + include/drt_host.h).
+
+The shared library is built in-tree by distributionraytracer_amd/csrc/Makefile (hipcc for the
+gfx950 kernels, g++ for the host scene library).  There is no fallback: if the library is
+missing, load() raises — the product never renders on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libdrt.so"
+CSRC = PKG / "csrc"
+
+DRT_OK = 0
+STATUS = {0: "DRT_OK", -1: "DRT_E_INVALID", -2: "DRT_E_HIP", -3: "DRT_E_NODEVICE", -4: "DRT_E_OOM",
+          -5: "DRT_E_STATE", -6: "DRT_E_UNSUPPORTED"}
+ACCEL = {"none": 0, "grid": 1, "bvh": 2}
+FRAME_STATS = 1
+
+_f = C.POINTER(C.c_float)
+_u8 = C.POINTER(C.c_uint8)
+_i32 = C.POINTER(C.c_int32)
+_u32 = C.POINTER(C.c_uint32)
+_i64 = C.POINTER(C.c_int64)
+_vp = C.c_void_p
+
+
+class DrtOptions(C.Structure):
+    _fields_ = [("device", C.c_int32), ("reserved", C.c_int32 * 7)]
+
+
+class DrtCamera(C.Structure):
+    _fields_ = [("eye", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3), ("n", C.c_float * 3),
+                ("w", C.c_float), ("h", C.c_float), ("plane_dist", C.c_float), ("focal_ratio", C.c_float),
+                ("aperture", C.c_float), ("res_x", C.c_int32), ("res_y", C.c_int32)]
+
+
+class DrtFrameParams(C.Structure):
+    _fields_ = [("seed", C.c_uint32), ("max_depth", C.c_int32), ("roughness", C.c_float), ("shard", C.c_int32),
+                ("n_shards", C.c_int32), ("tile", C.c_int32), ("flags", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
+class DrtFrameStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("closest_rays", "shadow_rays", "closest_inner", "closest_leaf",
+                                          "shadow_inner", "shadow_leaf", "closest_prims", "shadow_prims",
+                                          "samples")] + [("render_ms", C.c_double), ("kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_}
+
+
+class DrtSceneInfo(C.Structure):
+    _fields_ = [("res_x", C.c_int32), ("res_y", C.c_int32), ("spp", C.c_uint32), ("accel", C.c_int32),
+                ("n_objects", C.c_int32), ("n_lights", C.c_int32), ("n_materials", C.c_int32),
+                ("has_env", C.c_int32), ("skybox_loaded", C.c_int32), ("aperture", C.c_float),
+                ("bvh_nodes", C.c_int32), ("build_ms", C.c_double)]
+
+
+# Every symbol include/drt.h and include/drt_host.h declare, with its ctypes signature.
+SIGNATURES = {
+    # drt.h
+    "drt_abi_version": (C.c_int, []),
+    "drt_create": (C.c_int, [C.POINTER(_vp), C.POINTER(DrtOptions)]),
+    "drt_destroy": (None, [_vp]),
+    "drt_last_error": (C.c_char_p, [_vp]),
+    "drt_upload_scene": (C.c_int, [_vp, _vp]),
+    "drt_upload_bvh": (C.c_int, [_vp, _vp, C.c_uint32, _u32, C.c_uint32]),
+    "drt_upload_grid": (C.c_int, [_vp, _i32, _f, _f, _i64, _i32, C.c_int64]),
+    "drt_render": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _f]),
+    "drt_shard_layout": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _i64, _i64]),
+    "drt_render_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp]),
+    "drt_unshard_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp, _vp]),
+    "drt_trace_closest": (C.c_int, [_vp, _f, C.c_int32, _f, _f, _i32]),
+    "drt_trace_shadow": (C.c_int, [_vp, _f, C.c_int32, _u8]),
+    "drt_get_stats": (C.c_int, [_vp, C.POINTER(DrtFrameStats)]),
+    "drt_frame_times": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    # drt_host.h
+    "drt_scene_new": (_vp, []),
+    "drt_scene_load_p3f": (_vp, [C.c_char_p]),
+    "drt_scene_free": (None, [_vp]),
+    "drt_scene_info": (C.c_int, [_vp, C.POINTER(DrtSceneInfo)]),
+    "drt_scene_env": (C.c_char_p, [_vp]),
+    "drt_scene_set_skybox_face": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, _u8]),
+    "drt_scene_set_camera": (C.c_int, [_vp, _f, _f, _f, C.c_float, C.c_float, C.c_int, C.c_int, C.c_float,
+                                       C.c_float]),
+    "drt_scene_set_background": (C.c_int, [_vp, _f]),
+    "drt_scene_set_accel": (C.c_int, [_vp, C.c_int]),
+    "drt_scene_set_spp": (C.c_int, [_vp, C.c_uint32]),
+    "drt_scene_add_material": (C.c_int, [_vp, _f, C.c_double, _f, C.c_double, C.c_double, C.c_double, C.c_double]),
+    "drt_scene_use_material": (C.c_int, [_vp, C.c_int]),
+    "drt_scene_add_sphere": (C.c_int, [_vp, _f, C.c_float]),
+    "drt_scene_add_triangles": (C.c_int, [_vp, _f, C.c_int64]),
+    "drt_scene_add_plane_pts": (C.c_int, [_vp, _f, _f, _f]),
+    "drt_scene_add_plane_nd": (C.c_int, [_vp, _f, C.c_float]),
+    "drt_scene_add_box": (C.c_int, [_vp, _f, _f]),
+    "drt_scene_add_light_point": (C.c_int, [_vp, _f, _f]),
+    "drt_scene_add_light_quad": (C.c_int, [_vp, _f, _f, _f, _f, C.c_uint32]),
+    "drt_scene_build": (C.c_int, [_vp]),
+    "drt_scene_bvh_export": (C.c_int, [_vp, _f, _u32, _u32, _u32, _i32]),
+    "drt_scene_grid_export_dims": (C.c_int, [_vp, _i32, _f, _f, _i64]),
+    "drt_scene_grid_export": (C.c_int, [_vp, _i64, _i32]),
+    "drt_scene_camera_frame": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
+    "drt_scene_upload": (C.c_int, [_vp, _vp]),
+}
+
+
+def build(force: bool = False, jobs: int = 8) -> Path:
+    """Compile libdrt.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    args = ["make", "-C", str(CSRC), f"-j{jobs}"]
+    if force:
+        subprocess.run(["make", "-C", str(CSRC), "clean"], check=True, capture_output=True)
+    r = subprocess.run(args, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("libdrt.so build failed:\n" + r.stdout[-4000:] + r.stderr[-4000:])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def load():
+    """Load libdrt.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process.  PyTorch ships its own libamdhip64 (DT_NEEDED
+        # "libamdhip64.so", SONAME "libamdhip64.so.7"); loading torch first makes libdrt.so's
+        # DT_NEEDED "libamdhip64.so.7" resolve to that same runtime, so device pointers,
+        # streams and RCCL collectives from torch.distributed interoperate with our kernels.
+        import torch  # noqa: F401
+
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} is missing: run distributionraytracer_amd._lib.build() "
+                               "(make -C distributionraytracer_amd/csrc)")
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, ctx=None, what=""):
+    if rc != DRT_OK:
+        msg = ""
+        if ctx is not None:
+            try:
+                msg = load().drt_last_error(ctx).decode()
+            except Exception:
+                pass
+        raise RuntimeError(f"{what} failed: {STATUS.get(rc, rc)} {msg}".strip())

@@ -1,0 +1,584 @@
+// drt_capi.hip — the C ABI of include/drt.h: device memory, uploads, frame orchestration.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "drt_kernels.hpp"
+#include "drt_layout.hpp"
+
+namespace drt {
+void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats, hipStream_t st);
+void launch_reduce(const ReduceArgs& A, hipStream_t st);
+void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, int n_tiles, int n_shards,
+                    int tiles_per_shard, int res_x, int res_y, hipStream_t st);
+void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
+                  float* nrm, int32_t* obj, uint8_t* occ, hipStream_t st);
+}  // namespace drt
+
+using namespace drt;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {  // grow-only
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc(&p, n ? n : 16);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+}  // namespace
+
+struct drt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // per-frame HIP events (path-kernel start, path-kernel end / reduce start, frame end),
+  // a ring so every frame of a timed loop can be read back afterwards
+  static constexpr int kRing = 512;
+  std::vector<hipEvent_t> ring;
+  uint64_t frames = 0;
+  std::string err;
+  // scene
+  bool has_scene = false;
+  drt_camera cam{};
+  int accel = DRT_ACCEL_NONE;
+  uint32_t spp = 0;
+  float bg[3] = {0, 0, 0};
+  bool tri_only = true;
+  int n_prims = 0;
+  std::vector<PrimRecord> prims_scene;  // scene order
+  std::vector<drt_light> lights;
+  std::vector<drt_material> mats;
+  DevBuf d_prims, d_lights, d_mats, d_sky[6];
+  int has_sky = 0, sky_w[6] = {0}, sky_h[6] = {0}, sky_bpp[6] = {0};
+  // BVH
+  bool has_bvh = false;
+  DevBuf d_nodes, d_big;
+  float root_box[6] = {0};
+  uint32_t root_desc = 0;
+  int bvh_depth = 0;
+  // grid
+  bool has_grid = false;
+  int gdim[3] = {0, 0, 0};
+  float gmin[3] = {0}, gmax[3] = {0};
+  DevBuf d_cell_start, d_cell_objs;
+  // frame scratch
+  DevBuf d_samples, d_frame, d_stats, d_rays, d_out;
+  drt_frame_stats last{};
+  bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
+};
+
+#define DRT_FAIL(ctx, code, ...)                                        \
+  do {                                                                  \
+    char _b[512];                                                       \
+    snprintf(_b, sizeof(_b), __VA_ARGS__);                              \
+    (ctx)->err = _b;                                                    \
+    return (code);                                                      \
+  } while (0)
+#define DRT_HIP(ctx, expr)                                                                            \
+  do {                                                                                                \
+    hipError_t _e = (expr);                                                                           \
+    if (_e != hipSuccess) DRT_FAIL(ctx, _e == hipErrorOutOfMemory ? DRT_E_OOM : DRT_E_HIP, "%s: %s", \
+                                   #expr, hipGetErrorString(_e));                                     \
+  } while (0)
+
+static PrimRecord pack_prim(const drt_prim& p, uint32_t mat, uint32_t obj) {
+  PrimRecord r{};
+  float* q = r.q;
+  q[0] = p.a[0]; q[1] = p.a[1]; q[2] = p.a[2];
+  q[3] = bits_as_float((uint32_t)(p.type & 3) | (mat << 2));
+  q[7] = bits_as_float(obj);
+  switch (p.type) {
+    case DRT_PRIM_TRIANGLE:  // edge1 = P1 - P0, edge2 = P2 - P0 (scene.cpp:59-60)
+      q[4] = p.b[0] - p.a[0]; q[5] = p.b[1] - p.a[1]; q[6] = p.b[2] - p.a[2];
+      q[8] = p.c[0] - p.a[0]; q[9] = p.c[1] - p.a[1]; q[10] = p.c[2] - p.a[2];
+      break;
+    case DRT_PRIM_SPHERE:
+    case DRT_PRIM_PLANE:
+      q[4] = p.r;
+      break;
+    default:
+      q[4] = p.b[0]; q[5] = p.b[1]; q[6] = p.b[2];
+      break;
+  }
+  return r;
+}
+
+extern "C" {
+
+int drt_abi_version(void) { return DRT_ABI_VERSION; }
+
+int drt_create(drt_ctx** out, const drt_options* opt) {
+  if (!out) return DRT_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DRT_E_NODEVICE;
+  int dev = opt ? opt->device : 0;
+  if (dev < 0 || dev >= ndev) return DRT_E_INVALID;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return DRT_E_HIP;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DRT_E_NODEVICE;
+  drt_ctx* c = new drt_ctx();
+  c->device = dev;
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return DRT_E_HIP;
+  }
+  c->ring.assign(3 * drt_ctx::kRing, nullptr);
+  for (auto& e : c->ring)
+    if (hipEventCreate(&e) != hipSuccess) {
+      drt_destroy(c);
+      return DRT_E_HIP;
+    }
+  *out = c;
+  return DRT_OK;
+}
+
+void drt_destroy(drt_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& e : c->ring)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* drt_last_error(const drt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int drt_upload_scene(drt_ctx* c, const drt_scene_desc* s) {
+  if (!c || !s) return DRT_E_INVALID;
+  if (s->camera.res_x <= 0 || s->camera.res_y <= 0) DRT_FAIL(c, DRT_E_INVALID, "camera resolution must be positive");
+  if (s->n_prims < 0 || (s->n_prims > 0 && !s->prims)) DRT_FAIL(c, DRT_E_INVALID, "bad primitive array");
+  if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) DRT_FAIL(c, DRT_E_INVALID, "bad light array");
+  if (s->n_materials < 0 || (s->n_materials > 0 && !s->materials)) DRT_FAIL(c, DRT_E_INVALID, "bad material array");
+  if (s->accel < DRT_ACCEL_NONE || s->accel > DRT_ACCEL_BVH) DRT_FAIL(c, DRT_E_INVALID, "bad accel %d", s->accel);
+  DRT_HIP(c, hipSetDevice(c->device));
+  c->cam = s->camera;
+  c->accel = s->accel;
+  c->spp = s->spp;
+  memcpy(c->bg, s->background, sizeof(c->bg));
+  c->lights.assign(s->lights, s->lights + s->n_lights);
+  c->mats.assign(s->materials, s->materials + s->n_materials);
+  // Objects without a material are UB upstream (m_Material uninitialised); they get the
+  // default Material() (scene.h:38) appended at the end of the table.
+  const uint32_t dflt = (uint32_t)c->mats.size();
+  c->mats.push_back(drt_material{{0.2f, 0.2f, 0.2f}, 0.2f, {1.f, 1.f, 1.f}, 0.8f, 20.f, 1.0f, 0.0f, 1.0f});
+  c->n_prims = s->n_prims;
+  c->prims_scene.resize((size_t)s->n_prims);
+  c->tri_only = true;
+  for (int i = 0; i < s->n_prims; i++) {
+    const drt_prim& p = s->prims[i];
+    if (p.type < 0 || p.type > 3) DRT_FAIL(c, DRT_E_INVALID, "prim %d: bad type %d", i, p.type);
+    if (p.material >= s->n_materials) DRT_FAIL(c, DRT_E_INVALID, "prim %d: material %d out of range", i, p.material);
+    if (p.type != DRT_PRIM_TRIANGLE) c->tri_only = false;
+    c->prims_scene[i] = pack_prim(p, p.material < 0 ? dflt : (uint32_t)p.material, (uint32_t)i);
+  }
+  if (s->n_lights > 0 && !c->lights.empty())
+    for (auto& l : c->lights)
+      if (l.type != DRT_LIGHT_POINT && l.type != DRT_LIGHT_QUAD) DRT_FAIL(c, DRT_E_INVALID, "bad light type");
+  DRT_HIP(c, c->d_prims.ensure(sizeof(PrimRecord) * c->prims_scene.size()));
+  DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
+                       hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_lights.ensure(sizeof(drt_light) * std::max<size_t>(1, c->lights.size())));
+  if (!c->lights.empty())
+    DRT_HIP(c, hipMemcpy(c->d_lights.p, c->lights.data(), sizeof(drt_light) * c->lights.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_mats.ensure(sizeof(drt_material) * c->mats.size()));
+  DRT_HIP(c, hipMemcpy(c->d_mats.p, c->mats.data(), sizeof(drt_material) * c->mats.size(), hipMemcpyHostToDevice));
+  c->has_sky = s->has_skybox ? 1 : 0;
+  for (int f = 0; f < 6; f++) {
+    c->sky_w[f] = c->sky_h[f] = c->sky_bpp[f] = 0;
+    if (!c->has_sky) continue;
+    if (!s->skybox[f] || s->sky_w[f] <= 0 || s->sky_h[f] <= 0 || (s->sky_bpp[f] != 3 && s->sky_bpp[f] != 4))
+      DRT_FAIL(c, DRT_E_INVALID, "skybox face %d missing or malformed", f);
+    size_t n = (size_t)s->sky_w[f] * s->sky_h[f] * s->sky_bpp[f];
+    DRT_HIP(c, c->d_sky[f].ensure(n));
+    DRT_HIP(c, hipMemcpy(c->d_sky[f].p, s->skybox[f], n, hipMemcpyHostToDevice));
+    c->sky_w[f] = s->sky_w[f]; c->sky_h[f] = s->sky_h[f]; c->sky_bpp[f] = s->sky_bpp[f];
+  }
+  c->has_scene = true;
+  c->has_bvh = c->has_grid = false;
+  return DRT_OK;
+}
+
+int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, const uint32_t* order, uint32_t n_obj) {
+  if (!c || !nodes || n_nodes == 0) return DRT_E_INVALID;
+  if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its BVH");
+  if ((int)n_obj != c->n_prims || (n_obj && !order)) DRT_FAIL(c, DRT_E_INVALID, "object_order must cover all %d objects", c->n_prims);
+  std::vector<uint8_t> seen(n_obj, 0);
+  for (uint32_t i = 0; i < n_obj; i++) {
+    if (order[i] >= n_obj || seen[order[i]]) DRT_FAIL(c, DRT_E_INVALID, "object_order is not a permutation");
+    seen[order[i]] = 1;
+  }
+  // inner records in reference node order
+  std::vector<int64_t> rec(n_nodes, -1);
+  uint32_t n_inner = 0;
+  for (uint32_t i = 0; i < n_nodes; i++) {
+    const drt_bvh_node& nd = nodes[i];
+    if (nd.leaf) {
+      if ((uint64_t)nd.index + nd.n_objs > n_obj) DRT_FAIL(c, DRT_E_INVALID, "leaf %u out of range", i);
+    } else {
+      if ((uint64_t)nd.index + 1 >= n_nodes || nd.index <= i) DRT_FAIL(c, DRT_E_INVALID, "inner node %u: bad children", i);
+      rec[i] = n_inner++;
+    }
+  }
+  if (n_obj > kFirstMask) DRT_FAIL(c, DRT_E_UNSUPPORTED, "more than %u objects", kFirstMask);
+  std::vector<uint2> big;
+  auto desc_of = [&](uint32_t i) -> uint32_t {
+    const drt_bvh_node& nd = nodes[i];
+    if (!nd.leaf) return (uint32_t)rec[i];
+    if (nd.n_objs < kBigLeaf) return leaf_desc(nd.index, nd.n_objs);
+    big.push_back(make_uint2(nd.index, nd.n_objs));
+    return leaf_desc((uint32_t)big.size() - 1, kBigLeaf);
+  };
+  std::vector<NodeRecord> recs(n_inner);
+  for (uint32_t i = 0; i < n_nodes; i++) {
+    if (nodes[i].leaf) continue;
+    const drt_bvh_node& L = nodes[nodes[i].index];
+    const drt_bvh_node& R = nodes[nodes[i].index + 1];
+    NodeRecord& r = recs[rec[i]];
+    const float b[12] = {L.bmin[0], L.bmin[1], L.bmin[2], L.bmax[0], L.bmax[1], L.bmax[2],
+                         R.bmin[0], R.bmin[1], R.bmin[2], R.bmax[0], R.bmax[1], R.bmax[2]};
+    memcpy(r.box, b, sizeof(b));
+    r.desc[0] = desc_of(nodes[i].index);
+    r.desc[1] = desc_of(nodes[i].index + 1);
+    r.desc[2] = r.desc[3] = 0;
+  }
+  // depth (= bound on the traversal stack), iterative
+  int maxd = 0;
+  {
+    std::vector<std::pair<uint32_t, int>> st{{0u, 1}};
+    while (!st.empty()) {
+      auto [i, d] = st.back();
+      st.pop_back();
+      maxd = std::max(maxd, d);
+      if (!nodes[i].leaf) {
+        st.push_back({nodes[i].index, d + 1});
+        st.push_back({nodes[i].index + 1, d + 1});
+      }
+    }
+  }
+  if (maxd >= kMaxBvhDepth) DRT_FAIL(c, DRT_E_UNSUPPORTED, "BVH depth %d exceeds the %d-entry traversal stack", maxd, kMaxBvhDepth);
+  c->bvh_depth = maxd;
+  memcpy(c->root_box, nodes[0].bmin, 3 * sizeof(float));
+  memcpy(c->root_box + 3, nodes[0].bmax, 3 * sizeof(float));
+  c->root_desc = desc_of(0);
+  DRT_HIP(c, hipSetDevice(c->device));
+  DRT_HIP(c, c->d_nodes.ensure(sizeof(NodeRecord) * std::max<size_t>(1, recs.size())));
+  if (!recs.empty()) DRT_HIP(c, hipMemcpy(c->d_nodes.p, recs.data(), sizeof(NodeRecord) * recs.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_big.ensure(sizeof(uint2) * std::max<size_t>(1, big.size())));
+  if (!big.empty()) DRT_HIP(c, hipMemcpy(c->d_big.p, big.data(), sizeof(uint2) * big.size(), hipMemcpyHostToDevice));
+  // primitive records in BVH object order: every leaf is one contiguous run
+  std::vector<PrimRecord> perm(n_obj);
+  for (uint32_t i = 0; i < n_obj; i++) perm[i] = c->prims_scene[order[i]];
+  DRT_HIP(c, hipMemcpy(c->d_prims.p, perm.data(), sizeof(PrimRecord) * perm.size(), hipMemcpyHostToDevice));
+  c->has_bvh = true;
+  c->has_grid = false;
+  return DRT_OK;
+}
+
+int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], const float bmax[3], const int64_t* cs,
+                    const int32_t* co, int64_t n_refs) {
+  if (!c || !dims || !bmin || !bmax || !cs || (n_refs > 0 && !co)) return DRT_E_INVALID;
+  if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its grid");
+  if (dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0) DRT_FAIL(c, DRT_E_INVALID, "bad grid dims");
+  if (n_refs >= (int64_t)0xFFFFFFFF) DRT_FAIL(c, DRT_E_UNSUPPORTED, "too many grid references");
+  const size_t ncell = (size_t)dims[0] * dims[1] * dims[2];
+  std::vector<uint32_t> s32(ncell + 1), o32((size_t)n_refs);
+  for (size_t i = 0; i <= ncell; i++) {
+    if (cs[i] < 0 || cs[i] > n_refs || (i && cs[i] < cs[i - 1])) DRT_FAIL(c, DRT_E_INVALID, "bad cell_start");
+    s32[i] = (uint32_t)cs[i];
+  }
+  for (int64_t i = 0; i < n_refs; i++) {
+    if (co[i] < 0 || co[i] >= c->n_prims) DRT_FAIL(c, DRT_E_INVALID, "bad cell object");
+    o32[i] = (uint32_t)co[i];
+  }
+  DRT_HIP(c, hipSetDevice(c->device));
+  DRT_HIP(c, c->d_cell_start.ensure(4 * s32.size()));
+  DRT_HIP(c, hipMemcpy(c->d_cell_start.p, s32.data(), 4 * s32.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_cell_objs.ensure(4 * std::max<size_t>(1, o32.size())));
+  if (!o32.empty()) DRT_HIP(c, hipMemcpy(c->d_cell_objs.p, o32.data(), 4 * o32.size(), hipMemcpyHostToDevice));
+  // grid references index scene-order primitive records
+  DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
+                       hipMemcpyHostToDevice));
+  memcpy(c->gdim, dims, sizeof(c->gdim));
+  memcpy(c->gmin, bmin, sizeof(c->gmin));
+  memcpy(c->gmax, bmax, sizeof(c->gmax));
+  c->has_grid = true;
+  c->has_bvh = false;
+  return DRT_OK;
+}
+
+}  // extern "C"
+
+static int scene_args(drt_ctx* c, int accel, SceneArgs& S) {
+  memset(&S, 0, sizeof(S));
+  const drt_camera& k = c->cam;
+  memcpy(S.eye, k.eye, 12); memcpy(S.u, k.u, 12); memcpy(S.v, k.v, 12); memcpy(S.n, k.n, 12);
+  S.w = k.w; S.h = k.h; S.plane_dist = k.plane_dist; S.focal_ratio = k.focal_ratio; S.aperture = k.aperture;
+  S.res_x = k.res_x; S.res_y = k.res_y;
+  S.lights = c->d_lights.as<drt_light>();
+  S.n_lights = (int)c->lights.size();
+  S.mats = c->d_mats.as<drt_material>();
+  S.n_mats = (int)c->mats.size();
+  S.prims = c->d_prims.as<float4>();
+  S.n_prims = c->n_prims;
+  memcpy(S.bg, c->bg, 12);
+  S.has_sky = c->has_sky;
+  for (int f = 0; f < 6; f++) {
+    S.sky[f] = c->d_sky[f].as<uint8_t>();
+    S.sky_w[f] = c->sky_w[f]; S.sky_h[f] = c->sky_h[f]; S.sky_bpp[f] = c->sky_bpp[f];
+  }
+  if (accel == ACC_BVH) {
+    if (!c->has_bvh) DRT_FAIL(c, DRT_E_STATE, "scene uses a BVH but none was uploaded");
+    S.nodes = c->d_nodes.as<float4>();
+    memcpy(S.root_box, c->root_box, sizeof(S.root_box));
+    S.root_desc = c->root_desc;
+    S.big_leaves = c->d_big.as<uint2>();
+  } else if (accel == ACC_GRID) {
+    if (!c->has_grid) DRT_FAIL(c, DRT_E_STATE, "scene uses a grid but none was uploaded");
+    memcpy(S.gdim, c->gdim, sizeof(S.gdim));
+    memcpy(S.gmin, c->gmin, sizeof(S.gmin));
+    memcpy(S.gmax, c->gmax, sizeof(S.gmax));
+    S.cell_start = c->d_cell_start.as<uint32_t>();
+    S.cell_objs = c->d_cell_objs.as<uint32_t>();
+  }
+  return DRT_OK;
+}
+
+struct Plan {
+  FrameArgs F;
+  ReduceArgs R;
+  int tiles_y, n_tiles;
+};
+
+static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
+  if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
+  const int shards = p->n_shards <= 0 ? 1 : p->n_shards;
+  if (p->shard < 0 || p->shard >= shards) DRT_FAIL(c, DRT_E_INVALID, "shard %d of %d", p->shard, shards);
+  const int md = p->max_depth <= 0 ? 4 : p->max_depth;
+  if (md >= kMaxFrames) DRT_FAIL(c, DRT_E_UNSUPPORTED, "max_depth %d > %d", md, kMaxFrames - 1);
+  FrameArgs& F = P.F;
+  memset(&F, 0, sizeof(F));
+  F.seed = p->seed;
+  F.max_depth = md;
+  F.roughness = p->roughness;
+  F.spp = c->spp;
+  F.tile = p->tile > 0 ? p->tile : 16;
+  const int RX = c->cam.res_x, RY = c->cam.res_y;
+  F.tiles_x = (RX + F.tile - 1) / F.tile;
+  P.tiles_y = (RY + F.tile - 1) / F.tile;
+  P.n_tiles = F.tiles_x * P.tiles_y;
+  F.shard = p->shard;
+  F.n_shards = shards;
+  F.n_my_tiles = P.n_tiles > p->shard ? (P.n_tiles - p->shard + shards - 1) / shards : 0;
+  const bool AA = c->spp != 0;                           // main.cpp:1005-1010
+  F.dof = (c->cam.aperture != 0.0f && AA) ? 1 : 0;       // main.cpp:1013-1017
+  const bool seq = F.dof || p->roughness != 0.0f;
+  float scale = 1.0f;
+  const bool quad0 = !c->lights.empty() && c->lights[0].type == DRT_LIGHT_QUAD;
+  if (AA) {
+    F.n_sqrt = (int)std::sqrt((double)c->spp);
+    F.mode = seq ? MODE_SEQ : MODE_AA;
+    F.nsub = seq ? 1 : (int)c->spp;
+    scale = (float)(1.0 / (double)(float)c->spp);
+  } else if (quad0) {
+    F.grid_res = c->lights[0].grid_res;
+    F.grid_size = (int)std::sqrt((double)F.grid_res);
+    F.mode = seq ? MODE_SEQ : MODE_WHITTED_QUAD;
+    F.nsub = seq ? 1 : (int)F.grid_res;
+    scale = 1.0f / (float)(int)F.grid_res;
+  } else {
+    F.mode = seq ? MODE_SEQ : MODE_WHITTED_POINT;
+    F.nsub = 1;
+  }
+  const int per_pixel = F.mode == MODE_SEQ ? 1 : F.nsub;
+  F.n_items = (uint64_t)F.n_my_tiles * F.tile * F.tile * per_pixel;
+  ReduceArgs& R = P.R;
+  R.nsub = per_pixel;
+  R.scale = scale;
+  R.tile = F.tile; R.tiles_x = F.tiles_x; R.shard = F.shard; R.n_shards = F.n_shards; R.n_my_tiles = F.n_my_tiles;
+  R.res_x = RX; R.res_y = RY;
+  return DRT_OK;
+}
+
+static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool full_frame, hipStream_t st) {
+  Plan P;
+  int rc = plan_frame(c, p, P);
+  if (rc) return rc;
+  SceneArgs S;
+  rc = scene_args(c, c->accel, S);
+  if (rc) return rc;
+  DRT_HIP(c, hipSetDevice(c->device));
+  DRT_HIP(c, c->d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.F.n_items)));
+  DRT_HIP(c, c->d_stats.ensure(sizeof(unsigned long long) * ST_COUNT));
+  const bool stats = (p->flags & DRT_FRAME_STATS) != 0;
+  c->stats_valid = stats;
+  if (stats) DRT_HIP(c, hipMemsetAsync(c->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+  P.F.samples = c->d_samples.as<float4>();
+  P.F.stats = c->d_stats.as<unsigned long long>();
+  P.R.samples = P.F.samples;
+  P.R.full_frame = full_frame ? 1 : 0;
+  P.R.out = d_out;
+  hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
+  c->frames++;
+  DRT_HIP(c, hipEventRecord(ev[0], st));
+  if (P.F.n_items) launch_path(S, P.F, c->accel, c->tri_only, stats, st);
+  DRT_HIP(c, hipGetLastError());
+  DRT_HIP(c, hipEventRecord(ev[1], st));
+  if (P.F.n_my_tiles) launch_reduce(P.R, st);
+  DRT_HIP(c, hipGetLastError());
+  DRT_HIP(c, hipEventRecord(ev[2], st));
+  return DRT_OK;
+}
+
+extern "C" {
+
+int drt_shard_layout(const drt_ctx* c, const drt_frame_params* p, int64_t* tiles, int64_t* floats) {
+  if (!c || !p) return DRT_E_INVALID;
+  Plan P;
+  int rc = plan_frame(const_cast<drt_ctx*>(c), p, P);
+  if (rc) return rc;
+  const int shards = P.F.n_shards;
+  const int64_t per_shard = (P.n_tiles + shards - 1) / shards;  // equal-size shard buffers
+  if (tiles) *tiles = P.F.n_my_tiles;
+  if (floats) *floats = per_shard * P.F.tile * P.F.tile * 3;
+  return DRT_OK;
+}
+
+int drt_render_device(drt_ctx* c, const drt_frame_params* p, float* d_out, void* stream) {
+  if (!c || !p || !d_out) return DRT_E_INVALID;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  const bool full = (p->n_shards <= 1);
+  return run_frame(c, p, d_out, full, st);
+}
+
+int drt_unshard_device(drt_ctx* c, const drt_frame_params* p, const float* d_shards, float* d_frame, void* stream) {
+  if (!c || !p || !d_shards || !d_frame) return DRT_E_INVALID;
+  Plan P;
+  int rc = plan_frame(c, p, P);
+  if (rc) return rc;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  const int shards = P.F.n_shards;
+  const int per_shard = (P.n_tiles + shards - 1) / shards;
+  DRT_HIP(c, hipSetDevice(c->device));
+  launch_unshard(d_shards, d_frame, P.F.tile, P.F.tiles_x, P.n_tiles, shards, per_shard, c->cam.res_x, c->cam.res_y, st);
+  DRT_HIP(c, hipGetLastError());
+  return DRT_OK;
+}
+
+int drt_render(drt_ctx* c, const drt_frame_params* p, float* rgb_out) {
+  if (!c || !p || !rgb_out) return DRT_E_INVALID;
+  if (p->n_shards > 1) DRT_FAIL(c, DRT_E_INVALID, "drt_render renders whole frames; use drt_render_device for shards");
+  const size_t n = (size_t)c->cam.res_x * c->cam.res_y * 3;
+  DRT_HIP(c, hipSetDevice(c->device));
+  DRT_HIP(c, c->d_frame.ensure(sizeof(float) * n));
+  int rc = run_frame(c, p, c->d_frame.as<float>(), true, c->stream);
+  if (rc) return rc;
+  DRT_HIP(c, hipMemcpyAsync(rgb_out, c->d_frame.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  DRT_HIP(c, hipStreamSynchronize(c->stream));
+  return DRT_OK;
+}
+
+int drt_frame_times(drt_ctx* c, int max_frames, double* path_ms, double* total_ms) {
+  if (!c || max_frames < 0) return DRT_E_INVALID;
+  const uint64_t have = std::min<uint64_t>(c->frames, (uint64_t)drt_ctx::kRing);
+  const int n = (int)std::min<uint64_t>(have, (uint64_t)max_frames);
+  for (int i = 0; i < n; i++) {
+    const uint64_t f = c->frames - (uint64_t)n + (uint64_t)i;
+    hipEvent_t* ev = &c->ring[3 * (f % drt_ctx::kRing)];
+    DRT_HIP(c, hipEventSynchronize(ev[2]));
+    float a = 0, b = 0;
+    DRT_HIP(c, hipEventElapsedTime(&a, ev[0], ev[1]));
+    DRT_HIP(c, hipEventElapsedTime(&b, ev[0], ev[2]));
+    if (path_ms) path_ms[i] = a;
+    if (total_ms) total_ms[i] = b;
+  }
+  return n;
+}
+
+int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
+  if (!c || !out) return DRT_E_INVALID;
+  memset(&c->last, 0, sizeof(c->last));
+  if (c->frames > 0) {
+    hipEvent_t* ev = &c->ring[3 * ((c->frames - 1) % drt_ctx::kRing)];
+    DRT_HIP(c, hipSetDevice(c->device));
+    DRT_HIP(c, hipEventSynchronize(ev[2]));
+    float ms_k = 0, ms_all = 0;
+    DRT_HIP(c, hipEventElapsedTime(&ms_k, ev[0], ev[1]));
+    DRT_HIP(c, hipEventElapsedTime(&ms_all, ev[0], ev[2]));
+    c->last.kernel_ms = ms_k;
+    c->last.render_ms = ms_all;
+    if (c->stats_valid) {
+      unsigned long long s[ST_COUNT];
+      DRT_HIP(c, hipMemcpy(s, c->d_stats.p, sizeof(s), hipMemcpyDeviceToHost));
+      c->last.closest_rays = s[ST_CLOSEST]; c->last.shadow_rays = s[ST_SHADOW];
+      c->last.closest_inner = s[ST_C_INNER]; c->last.closest_leaf = s[ST_C_LEAF];
+      c->last.shadow_inner = s[ST_S_INNER]; c->last.shadow_leaf = s[ST_S_LEAF];
+      c->last.closest_prims = s[ST_C_PRIMS]; c->last.shadow_prims = s[ST_S_PRIMS];
+      c->last.samples = s[ST_SAMPLES];
+    }
+  }
+  *out = c->last;
+  return DRT_OK;
+}
+
+static int trace_common(drt_ctx* c, const float* rays, int32_t n, int shadow, float* t, float* nrm, int32_t* obj,
+                        uint8_t* occ) {
+  if (!c || n < 0 || (n > 0 && !rays)) return DRT_E_INVALID;
+  if (n == 0) return DRT_OK;
+  SceneArgs S;
+  if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
+  int rc = scene_args(c, c->accel, S);
+  if (rc) return rc;
+  DRT_HIP(c, hipSetDevice(c->device));
+  const size_t rb = sizeof(float) * 6 * (size_t)n;
+  const size_t ob = shadow ? (size_t)n : (sizeof(float) * 4 + sizeof(int32_t)) * (size_t)n;
+  DRT_HIP(c, c->d_rays.ensure(rb));
+  DRT_HIP(c, c->d_out.ensure(ob));
+  DRT_HIP(c, hipMemcpyAsync(c->d_rays.p, rays, rb, hipMemcpyHostToDevice, c->stream));
+  float* dt = c->d_out.as<float>();
+  float* dn = dt + n;
+  int32_t* dobj = (int32_t*)(dn + 3 * (size_t)n);
+  uint8_t* docc = c->d_out.as<uint8_t>();
+  launch_trace(S, c->accel, c->tri_only, c->d_rays.as<float>(), n, shadow, dt, dn, dobj, docc, c->stream);
+  DRT_HIP(c, hipGetLastError());
+  if (shadow) {
+    DRT_HIP(c, hipMemcpyAsync(occ, docc, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    DRT_HIP(c, hipMemcpyAsync(t, dt, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    DRT_HIP(c, hipMemcpyAsync(nrm, dn, sizeof(float) * 3 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    DRT_HIP(c, hipMemcpyAsync(obj, dobj, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  }
+  DRT_HIP(c, hipStreamSynchronize(c->stream));
+  return DRT_OK;
+}
+
+int drt_trace_closest(drt_ctx* c, const float* rays, int32_t n, float* t, float* nrm, int32_t* obj) {
+  if (!t || !nrm || !obj) return DRT_E_INVALID;
+  return trace_common(c, rays, n, 0, t, nrm, obj, nullptr);
+}
+
+int drt_trace_shadow(drt_ctx* c, const float* rays, int32_t n, uint8_t* occ) {
+  if (!occ) return DRT_E_INVALID;
+  return trace_common(c, rays, n, 1, nullptr, nullptr, nullptr, occ);
+}
+
+}  // extern "C"

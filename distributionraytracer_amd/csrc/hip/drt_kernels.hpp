@@ -1,0 +1,81 @@
+// drt_kernels.hpp — kernel argument blocks shared by drt_kernels.hip and drt_capi.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/drt.h"
+
+namespace drt {
+
+enum Accel : int { ACC_NONE = 0, ACC_GRID = 1, ACC_BVH = 2 };
+
+enum FrameMode : int {
+  MODE_AA = 0,            // one thread per (pixel, sample): main.cpp:618-671 without DoF/roughness
+  MODE_SEQ = 1,           // one thread per pixel, samples in order with the keyed RNG stream
+  MODE_WHITTED_QUAD = 2,  // one thread per (pixel, regular light sample): main.cpp:683-697
+  MODE_WHITTED_POINT = 3  // one thread per pixel: main.cpp:698-701
+};
+
+enum StatSlot : int {
+  ST_CLOSEST = 0, ST_SHADOW, ST_C_INNER, ST_C_LEAF, ST_S_INNER, ST_S_LEAF, ST_C_PRIMS, ST_S_PRIMS, ST_SAMPLES,
+  ST_COUNT
+};
+
+constexpr int kMaxFrames = 16;     // max_depth <= 15
+constexpr int kMaxBvhDepth = 96;   // traversal stack entries (host rejects deeper trees)
+
+struct SceneArgs {
+  // Camera (camera.h:32-61), precomputed on the host
+  float eye[3], u[3], v[3], n[3];
+  float w, h, plane_dist, focal_ratio, aperture;
+  int res_x, res_y;
+  const drt_light* lights;
+  int n_lights;
+  const drt_material* mats;
+  int n_mats;
+  const float4* prims;
+  int n_prims;
+  float bg[3];
+  int has_sky;
+  const uint8_t* sky[6];
+  int sky_w[6], sky_h[6], sky_bpp[6];
+  // BVH
+  const float4* nodes;
+  float root_box[6];
+  uint32_t root_desc;
+  const uint2* big_leaves;
+  // Grid
+  int gdim[3];
+  float gmin[3], gmax[3];
+  const uint32_t* cell_start;
+  const uint32_t* cell_objs;
+};
+
+struct FrameArgs {
+  uint32_t seed;
+  int max_depth;
+  float roughness;
+  int mode;
+  int dof;
+  uint32_t spp;
+  int n_sqrt;         // (int)sqrt(spp)        (main.cpp:619)
+  int nsub;           // work items per pixel
+  uint32_t grid_res;  // light 0 gridRes       (main.cpp:684)
+  int grid_size;      // (int)sqrt(gridRes)    (main.cpp:689)
+  int tile, tiles_x, shard, n_shards, n_my_tiles;
+  uint64_t n_items;
+  float4* samples;
+  unsigned long long* stats;
+};
+
+struct ReduceArgs {
+  const float4* samples;
+  int nsub;
+  float scale;  // (float)(1.0/spp) for AA (main.cpp:666), 1.0f/gridRes (main.cpp:696), 1 otherwise
+  int tile, tiles_x, shard, n_shards, n_my_tiles;
+  int res_x, res_y;
+  int full_frame;  // write the (x, y) frame, else the shard-compact buffer
+  float* out;
+};
+
+}  // namespace drt

@@ -1,0 +1,203 @@
+// drt_host_capi.cpp — C entry points (include/drt_host.h) over the C++ host scene API.
+#include <cstring>
+
+#include "../../../include/drt_host.h"
+#include "drt_scene.hpp"
+
+using namespace drt;
+
+struct drt_scene {
+  Scene scene;
+  BVH bvh;
+  Grid grid;
+  Material* current = nullptr;
+  bool built = false;
+};
+
+static Vector v3(const float* p) { return Vector(p[0], p[1], p[2]); }
+
+extern "C" {
+
+drt_scene* drt_scene_new(void) { return new drt_scene(); }
+
+drt_scene* drt_scene_load_p3f(const char* path) {
+  if (!path) return nullptr;
+  drt_scene* s = new drt_scene();
+  if (!s->scene.load_p3f(path)) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void drt_scene_free(drt_scene* s) { delete s; }
+
+int drt_scene_info(const drt_scene* s, drt_scene_info_t* o) {
+  if (!s || !o) return DRT_E_INVALID;
+  memset(o, 0, sizeof(*o));
+  Scene& sc = const_cast<Scene&>(s->scene);
+  if (Camera* c = sc.GetCamera()) {
+    o->res_x = c->GetResX();
+    o->res_y = c->GetResY();
+    o->aperture = c->GetAperture();
+  }
+  o->spp = sc.GetSamplesPerPixel();
+  o->accel = sc.GetAccelStruct() == BVH_ACC ? DRT_ACCEL_BVH : (sc.GetAccelStruct() == GRID_ACC ? DRT_ACCEL_GRID : DRT_ACCEL_NONE);
+  o->n_objects = sc.getNumObjects();
+  o->n_lights = sc.getNumLights();
+  drt_scene_desc d;
+  std::vector<drt_prim> p;
+  std::vector<drt_light> l;
+  std::vector<drt_material> m;
+  o->n_materials = 0;
+  sc.describe(d, p, l, m);
+  o->n_materials = (int32_t)m.size();
+  o->has_env = sc.GetSkyBoxFlg() ? 1 : 0;
+  o->skybox_loaded = sc.SkyboxComplete() ? 1 : 0;
+  o->bvh_nodes = (int32_t)s->bvh.nodeList().size();
+  o->build_ms = o->accel == DRT_ACCEL_GRID ? s->grid.build_ms : s->bvh.build_ms;
+  return DRT_OK;
+}
+
+const char* drt_scene_env(const drt_scene* s) { return s ? s->scene.GetSkyboxDir().c_str() : ""; }
+
+int drt_scene_set_skybox_face(drt_scene* s, int face, int w, int h, int bpp, const uint8_t* px) {
+  if (!s || !px || face < 0 || face > 5 || w <= 0 || h <= 0 || (bpp != 3 && bpp != 4)) return DRT_E_INVALID;
+  s->scene.SetSkyboxFace(face, w, h, bpp, px);
+  return DRT_OK;
+}
+
+int drt_scene_set_camera(drt_scene* s, const float eye[3], const float at[3], const float up[3], float fovy,
+                         float hither, int rx, int ry, float ap, float fr) {
+  if (!s || rx <= 0 || ry <= 0) return DRT_E_INVALID;
+  s->scene.SetCamera(new Camera(v3(eye), v3(at), v3(up), fovy, hither, (float)(1000.0 * hither), rx, ry, ap, fr));
+  return DRT_OK;
+}
+
+int drt_scene_set_background(drt_scene* s, const float rgb[3]) {
+  if (!s) return DRT_E_INVALID;
+  s->scene.SetBackgroundColor(Color(rgb[0], rgb[1], rgb[2]));
+  return DRT_OK;
+}
+
+int drt_scene_set_accel(drt_scene* s, int a) {
+  if (!s || a < 0 || a > 2) return DRT_E_INVALID;
+  s->scene.SetAccelStruct(a == DRT_ACCEL_BVH ? BVH_ACC : (a == DRT_ACCEL_GRID ? GRID_ACC : NONE));
+  s->built = false;
+  return DRT_OK;
+}
+
+int drt_scene_set_spp(drt_scene* s, uint32_t spp) {
+  if (!s) return DRT_E_INVALID;
+  s->scene.SetSamplesPerPixel(spp);
+  return DRT_OK;
+}
+
+int drt_scene_add_material(drt_scene* s, const float d[3], double kd, const float sp[3], double ks, double shine,
+                           double t, double ior) {
+  if (!s) return DRT_E_INVALID;
+  s->current = s->scene.addMaterial(
+      Material(Color(d[0], d[1], d[2]), (float)kd, Color(sp[0], sp[1], sp[2]), (float)ks, (float)shine, (float)t, (float)ior));
+  return s->current->index;
+}
+
+int drt_scene_use_material(drt_scene* s, int m) {
+  (void)s; (void)m;
+  return DRT_E_UNSUPPORTED;  // materials apply to the objects that follow them, as in P3F
+}
+
+static int add(drt_scene* s, Object* o) {
+  if (s->current) o->SetMaterial(s->current);
+  s->scene.addObject(o);
+  s->built = false;
+  return s->scene.getNumObjects() - 1;
+}
+
+int drt_scene_add_sphere(drt_scene* s, const float c[3], float r) { return s ? add(s, new Sphere(v3(c), r)) : DRT_E_INVALID; }
+int drt_scene_add_plane_pts(drt_scene* s, const float a[3], const float b[3], const float c[3]) {
+  return s ? add(s, new Plane(v3(a), v3(b), v3(c))) : DRT_E_INVALID;
+}
+int drt_scene_add_plane_nd(drt_scene* s, const float n[3], float d) { return s ? add(s, new Plane(v3(n), d)) : DRT_E_INVALID; }
+int drt_scene_add_box(drt_scene* s, const float a[3], const float b[3]) { return s ? add(s, new aaBox(v3(a), v3(b))) : DRT_E_INVALID; }
+int drt_scene_add_triangles(drt_scene* s, const float* v, int64_t n) {
+  if (!s || n < 0 || (n && !v)) return DRT_E_INVALID;
+  s->scene.addTriangles(v, (size_t)n, s->current);
+  s->built = false;
+  return s->scene.getNumObjects() - 1;
+}
+int drt_scene_add_light_point(drt_scene* s, const float p[3], const float c[3]) {
+  if (!s) return DRT_E_INVALID;
+  s->scene.addLight(new Light(v3(p), Color(c[0], c[1], c[2])));
+  return s->scene.getNumLights() - 1;
+}
+int drt_scene_add_light_quad(drt_scene* s, const float p[3], const float c[3], const float a[3], const float b[3],
+                             uint32_t g) {
+  if (!s) return DRT_E_INVALID;
+  s->scene.addLight(new Light(v3(p), Color(c[0], c[1], c[2]), v3(a), v3(b), g));
+  return s->scene.getNumLights() - 1;
+}
+
+int drt_scene_build(drt_scene* s) {  // main.cpp:1023-1049
+  if (!s) return DRT_E_INVALID;
+  std::vector<Object*> objs = s->scene.objectList();
+  if (s->scene.GetAccelStruct() == BVH_ACC) s->bvh.Build(objs);
+  else if (s->scene.GetAccelStruct() == GRID_ACC) s->grid.Build(objs);
+  s->built = true;
+  return DRT_OK;
+}
+
+int drt_scene_bvh_export(const drt_scene* s, float* boxes, uint32_t* leaf, uint32_t* index, uint32_t* nobjs,
+                         int32_t* order) {
+  if (!s) return DRT_E_INVALID;
+  const auto& nd = s->bvh.nodeList();
+  for (size_t i = 0; i < nd.size(); i++) {
+    const AABB& b = nd[i].bbox;
+    float* o = boxes + 6 * i;
+    o[0] = b.min.x; o[1] = b.min.y; o[2] = b.min.z; o[3] = b.max.x; o[4] = b.max.y; o[5] = b.max.z;
+    leaf[i] = nd[i].leaf;
+    index[i] = nd[i].index;
+    nobjs[i] = nd[i].leaf ? nd[i].n_objs : 0;
+  }
+  const auto& ob = s->bvh.objectOrder();
+  for (size_t i = 0; i < ob.size(); i++) order[i] = ob[i]->scene_index;
+  return DRT_OK;
+}
+
+int drt_scene_grid_export_dims(const drt_scene* s, int32_t dims[3], float bmin[3], float bmax[3], int64_t* n_refs) {
+  if (!s) return DRT_E_INVALID;
+  const Grid& g = s->grid;
+  dims[0] = g.nx; dims[1] = g.ny; dims[2] = g.nz;
+  bmin[0] = g.bbox.min.x; bmin[1] = g.bbox.min.y; bmin[2] = g.bbox.min.z;
+  bmax[0] = g.bbox.max.x; bmax[1] = g.bbox.max.y; bmax[2] = g.bbox.max.z;
+  *n_refs = (int64_t)g.cell_objs.size();
+  return DRT_OK;
+}
+
+int drt_scene_grid_export(const drt_scene* s, int64_t* cs, int32_t* co) {
+  if (!s) return DRT_E_INVALID;
+  memcpy(cs, s->grid.cell_start.data(), sizeof(int64_t) * s->grid.cell_start.size());
+  memcpy(co, s->grid.cell_objs.data(), sizeof(int32_t) * s->grid.cell_objs.size());
+  return DRT_OK;
+}
+
+int drt_scene_camera_frame(const drt_scene* s, drt_camera* out) {
+  if (!s || !out) return DRT_E_INVALID;
+  Camera* c = const_cast<Scene&>(s->scene).GetCamera();
+  if (!c) return DRT_E_STATE;
+  *out = c->frame();
+  return DRT_OK;
+}
+
+int drt_scene_upload(drt_ctx* ctx, drt_scene* s) {
+  if (!ctx || !s) return DRT_E_INVALID;
+  if (!s->scene.GetCamera()) return DRT_E_STATE;
+  if (s->scene.GetSkyBoxFlg() && !s->scene.SkyboxComplete()) return DRT_E_STATE;
+  if (!s->built) drt_scene_build(s);
+  int rc = upload_scene(ctx, s->scene, &s->bvh, &s->grid);
+  if (rc) return rc;
+  s->bvh.bind(ctx, &s->scene);
+  s->grid.bind(ctx, &s->scene);
+  return DRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+/*
+ * drt.h — C ABI of the MI355X distribution ray tracer (libdrt.so).
+ *
+ * This is the drop-in boundary for the reference's hot path (rita-mota/DistributionRayTracer,
+ * paths relative to DistributionRayTracer/).  The reference has no FFI: its hot path is the
+ * C++ class API called from main.cpp.  Each entry point below names the reference interface
+ * it replaces:
+ *
+ *   drt_upload_scene   <- Scene / Camera / Light / Material / Object state read by
+ *                         rayTracing() (scene.h:24-231, camera.h:12-101)
+ *   drt_upload_bvh     <- BVH::Build result (rayAccelerator.h:87-94, bvh.cpp:27-227)
+ *   drt_upload_grid    <- Grid::Build result (rayAccelerator.h:12-37, grid.cpp:30-97)
+ *   drt_trace_closest  <- BVH::Traverse(Ray&, Object**, HitRecord&)  (bvh.cpp:231-314)
+ *                         Grid::Traverse(Ray&, Object**, HitRecord&) (grid.cpp:247-306)
+ *                         the NONE linear scan                       (main.cpp:310-336)
+ *   drt_trace_shadow   <- BVH::Traverse(Ray&) (bvh.cpp:316-391), Grid::Traverse(Ray&)
+ *                         (grid.cpp:309-358)
+ *   drt_render         <- renderScene() zone B (main.cpp:525-738) incl. rayTracing()
+ *                         (main.cpp:294-521): jittered AA, light-sample shuffle, thin-lens
+ *                         DoF, Whitted area-light grid, Phong + shadows, refraction/reflection
+ *
+ * Conventions: plain C types only; caller owns all host memory; the context owns all device
+ * memory.  Every function returns 0 (DRT_OK) or a negative drt_status and never exits the
+ * process; drt_last_error() describes the last failure.  One host thread per context.
+ * Calls are blocking except drt_render_device, which is asynchronous on the given stream.
+ *
+ * Frame buffer layout (main.cpp:705-714): float RGB, index 3*(x + RES_X*y), row y = 0 is the
+ * BOTTOM row of the image (OpenGL / DevIL lower-left origin).
+ *
+ * RNG: the reference uses CRT rand() seeded with time()^2; parity is defined on the keyed
+ * stream of SURVEY.md §8c — the k-th rand() call inside pixel P = y*RES_X + x returns
+ * mix32(seed ^ mix32(P*0x9E3779B9 ^ mix32(k))) >> 17, RAND_MAX = 0x7FFF.
+ */
+#ifndef DRT_H
+#define DRT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRT_ABI_VERSION 1
+
+typedef enum {
+  DRT_OK = 0,
+  DRT_E_INVALID = -1,     /* bad argument / malformed scene                         */
+  DRT_E_HIP = -2,         /* HIP runtime error                                        */
+  DRT_E_NODEVICE = -3,    /* no usable gfx950 device                                  */
+  DRT_E_OOM = -4,         /* device allocation failed                                 */
+  DRT_E_STATE = -5,       /* call order (e.g. render before upload)                   */
+  DRT_E_UNSUPPORTED = -6  /* feature outside this build                               */
+} drt_status;
+
+enum { DRT_ACCEL_NONE = 0, DRT_ACCEL_GRID = 1, DRT_ACCEL_BVH = 2 };               /* scene.h:22 */
+enum { DRT_PRIM_TRIANGLE = 0, DRT_PRIM_SPHERE = 1, DRT_PRIM_PLANE = 2, DRT_PRIM_BOX = 3 };
+enum { DRT_LIGHT_POINT = 0, DRT_LIGHT_QUAD = 1 };                                  /* scene.h:16 */
+
+typedef struct drt_ctx drt_ctx;
+
+typedef struct {
+  int32_t device;       /* HIP device ordinal                                        */
+  int32_t reserved[7];
+} drt_options;
+
+/* Camera frame exactly as the host Camera constructor computes it (camera.h:32-61). */
+typedef struct {
+  float eye[3], u[3], v[3], n[3];
+  float w, h, plane_dist, focal_ratio, aperture;
+  int32_t res_x, res_y;
+} drt_camera;
+
+/* Light (scene.h:68-107): quad lights span pos + e1*s + e2*t. */
+typedef struct {
+  int32_t type;
+  float pos[3];
+  float e1[3], e2[3];
+  uint32_t grid_res;
+} drt_light;
+
+/* Material (scene.h:34-66); refl is m_Refl (= Ks for P3F materials, scene.h:42). */
+typedef struct {
+  float diff[3];
+  float kd;
+  float spec[3];
+  float ks, shine, refl, trans, ior;
+} drt_material;
+
+/* Object (scene.h:109-180).  triangle: a,b,c = P0,P1,P2; sphere: a = centre, r = radius;
+ * plane: a = PN, r = D; box: a = min, b = max.  material < 0 = none (reference UB). */
+typedef struct {
+  int32_t type;
+  int32_t material;
+  float a[3], b[3], c[3];
+  float r;
+} drt_prim;
+
+typedef struct {
+  drt_camera camera;
+  const drt_material* materials;
+  int32_t n_materials;
+  const drt_prim* prims;
+  int32_t n_prims;
+  const drt_light* lights;
+  int32_t n_lights;
+  float background[3];          /* bclr (scene.cpp:680)                                  */
+  int32_t accel;                /* DRT_ACCEL_*                                           */
+  uint32_t spp;                 /* 0 = Whitted (main.cpp:1005-1010)                      */
+  int32_t has_skybox;           /* env (scene.cpp:687)                                   */
+  const uint8_t* skybox[6];     /* faces RIGHT..BACK, rows bottom-up (scene.cpp:345)     */
+  int32_t sky_w[6], sky_h[6], sky_bpp[6];
+} drt_scene_desc;
+
+/* One BVHNode (rayAccelerator.h:50-67) in the reference's node numbering: inner nodes keep
+ * their two children at index and index+1 (bvh.cpp:206-222); leaves cover
+ * object_order[index .. index+n_objs). */
+typedef struct {
+  float bmin[3], bmax[3];
+  uint32_t leaf;
+  uint32_t index;
+  uint32_t n_objs;
+} drt_bvh_node;
+
+enum { DRT_FRAME_STATS = 1 };
+
+typedef struct {
+  uint32_t seed;       /* keyed-RNG seed                                                */
+  int32_t max_depth;   /* MAX_DEPTH (main.cpp:34) = 4                                   */
+  float roughness;     /* roughness_param (main.cpp:507) = 0                            */
+  int32_t shard;       /* this rank's shard: tiles t with t % n_shards == shard        */
+  int32_t n_shards;    /* 1 = whole frame                                               */
+  int32_t tile;        /* tile edge in pixels (0 -> 16)                                 */
+  int32_t flags;       /* DRT_FRAME_STATS: count rays / node visits / prim tests        */
+  int32_t reserved[5];
+} drt_frame_params;
+
+typedef struct {
+  uint64_t closest_rays, shadow_rays;     /* Traverse() calls                            */
+  uint64_t closest_inner, closest_leaf;   /* node-loop iterations (bvh.cpp:245)           */
+  uint64_t shadow_inner, shadow_leaf;     /* (bvh.cpp:331)                                */
+  uint64_t closest_prims, shadow_prims;   /* Object::hit calls                           */
+  uint64_t samples;                       /* rayTracing(depth = 1) calls                 */
+  double render_ms;                        /* device time of the last drt_render*        */
+  double kernel_ms;                        /* device time of the path-tracing kernel     */
+} drt_frame_stats;
+
+int drt_create(drt_ctx** out, const drt_options* opt);
+void drt_destroy(drt_ctx* ctx);
+const char* drt_last_error(const drt_ctx* ctx);
+int drt_abi_version(void);
+
+int drt_upload_scene(drt_ctx* ctx, const drt_scene_desc* scene);
+int drt_upload_bvh(drt_ctx* ctx, const drt_bvh_node* nodes, uint32_t n_nodes, const uint32_t* object_order,
+                   uint32_t n_objects);
+int drt_upload_grid(drt_ctx* ctx, const int32_t dims[3], const float bmin[3], const float bmax[3],
+                    const int64_t* cell_start /* nx*ny*nz+1 */, const int32_t* cell_objs, int64_t n_refs);
+
+/* Whole frame into host memory (RES_Y*RES_X*3 floats). */
+int drt_render(drt_ctx* ctx, const drt_frame_params* params, float* rgb_out);
+
+/* Tile-sharded frame into DEVICE memory, asynchronous on `hip_stream` (a hipStream_t, NULL =
+ * the context's stream).  With n_shards == 1 the output is the full frame; otherwise it is
+ * the shard-compact tile buffer of drt_shard_layout(). */
+int drt_shard_layout(const drt_ctx* ctx, const drt_frame_params* params, int64_t* tiles_in_shard,
+                     int64_t* floats_per_shard);
+int drt_render_device(drt_ctx* ctx, const drt_frame_params* params, float* d_out, void* hip_stream);
+/* Reassemble n_shards shard-compact buffers (laid end to end, floats_per_shard apart) into a
+ * full device frame. */
+int drt_unshard_device(drt_ctx* ctx, const drt_frame_params* params, const float* d_shards, float* d_frame,
+                       void* hip_stream);
+
+/* Batched ray queries against the uploaded scene (rays: n x {ox,oy,oz,dx,dy,dz}).
+ * closest: t (FLT_MAX on miss), the HitRecord normal, object index (-1 on miss).
+ * shadow: 1 if occluded, with the accelerator's own range rule. */
+int drt_trace_closest(drt_ctx* ctx, const float* rays, int32_t n, float* t, float* normal, int32_t* object);
+int drt_trace_shadow(drt_ctx* ctx, const float* rays, int32_t n, uint8_t* occluded);
+
+/* Counters (frames rendered with DRT_FRAME_STATS) and device times of the most recent frame;
+ * waits for that frame. */
+int drt_get_stats(drt_ctx* ctx, drt_frame_stats* out);
+
+/* Device durations of the most recent min(max_frames, 512) frames, oldest first: the
+ * path-tracing kernel (path_ms) and kernel + reduce (total_ms), from HIP events recorded on the
+ * stream each frame ran on.  Waits for those frames.  Returns the count written (>= 0). */
+int drt_frame_times(drt_ctx* ctx, int max_frames, double* path_ms, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,76 @@
+/*
+ * drt_host.h — C ABI of the host-side scene library (also in libdrt.so).
+ *
+ * Flat C entry points over the C++ host API (distributionraytracer_amd/csrc/host/
+ * drt_scene.hpp), for callers that cannot use C++ (Python ctypes, other FFIs):
+ *
+ *   drt_scene_load_p3f     <- Scene::load_p3f            (scene.cpp:474-740)
+ *   drt_scene_set_camera   <- Camera::Camera             (camera.h:32-61)
+ *   drt_scene_add_*        <- Scene::addObject / addLight and the Sphere/Triangle/Plane/aaBox/
+ *                             Light/Material constructors (scene.h:34-180)
+ *   drt_scene_build        <- main.cpp:1023-1049: BVH::Build / Grid::Build (bvh.cpp:27-227,
+ *                             grid.cpp:30-97), tree-identical to the reference
+ *   drt_scene_upload       <- the hand-off renderScene() relied on through globals
+ *                             (main.cpp:79-93): scene + accelerator into a drt_ctx
+ *
+ * Conventions as in drt.h: 0 / negative drt_status, caller-owned host memory.
+ */
+#ifndef DRT_HOST_H
+#define DRT_HOST_H
+#include <stdint.h>
+
+#include "drt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct drt_scene drt_scene;
+
+typedef struct {
+  int32_t res_x, res_y;
+  uint32_t spp;
+  int32_t accel;
+  int32_t n_objects, n_lights, n_materials;
+  int32_t has_env, skybox_loaded;
+  float aperture;
+  int32_t bvh_nodes;
+  double build_ms;
+} drt_scene_info_t;
+
+drt_scene* drt_scene_new(void);
+drt_scene* drt_scene_load_p3f(const char* path);
+void drt_scene_free(drt_scene* s);
+int drt_scene_info(const drt_scene* s, drt_scene_info_t* out);
+const char* drt_scene_env(const drt_scene* s);
+int drt_scene_set_skybox_face(drt_scene* s, int face, int w, int h, int bpp, const uint8_t* bottom_up_rgb);
+int drt_scene_set_camera(drt_scene* s, const float eye[3], const float at[3], const float up[3], float fovy,
+                         float hither, int res_x, int res_y, float aperture_ratio, float focal_ratio);
+int drt_scene_set_background(drt_scene* s, const float rgb[3]);
+int drt_scene_set_accel(drt_scene* s, int accel);
+int drt_scene_set_spp(drt_scene* s, uint32_t spp);
+int drt_scene_add_material(drt_scene* s, const float diff[3], double kd, const float spec[3], double ks,
+                           double shine, double t, double ior);
+int drt_scene_use_material(drt_scene* s, int mat);
+int drt_scene_add_sphere(drt_scene* s, const float c[3], float r);
+int drt_scene_add_triangles(drt_scene* s, const float* verts, int64_t n);
+int drt_scene_add_plane_pts(drt_scene* s, const float p0[3], const float p1[3], const float p2[3]);
+int drt_scene_add_plane_nd(drt_scene* s, const float n[3], float d);
+int drt_scene_add_box(drt_scene* s, const float mn[3], const float mx[3]);
+int drt_scene_add_light_point(drt_scene* s, const float pos[3], const float rgb[3]);
+int drt_scene_add_light_quad(drt_scene* s, const float pos[3], const float rgb[3], const float v1[3],
+                             const float v2[3], uint32_t grid_res);
+
+int drt_scene_build(drt_scene* s);
+int drt_scene_bvh_export(const drt_scene* s, float* boxes, uint32_t* leaf, uint32_t* index, uint32_t* nobjs,
+                         int32_t* object_order);
+int drt_scene_grid_export_dims(const drt_scene* s, int32_t dims[3], float bmin[3], float bmax[3], int64_t* n_refs);
+int drt_scene_grid_export(const drt_scene* s, int64_t* cell_start, int32_t* cell_objs);
+int drt_scene_camera_frame(const drt_scene* s, drt_camera* out);
+
+int drt_scene_upload(drt_ctx* ctx, drt_scene* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

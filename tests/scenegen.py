@@ -114,3 +114,19 @@ def write(tmp_path, name, text):
     p = tmp_path / name
     p.write_text(text)
     return p
+
+
+def balls_low_text(res=(512, 512), spp=16, accel="none"):
+    """The geometry, lights and materials of P3D_Scenes/balls_low.p3f,
+    with resolution / spp / accel as parameters."""
+    lines = header(res=res, spp=spp, accel=accel)
+    lines += ["light quad 4 3 2 1 1 1 4 2 2 3 3 2 16", "light quad 1 -4 4 1 1 1 0 -4 4 1 -3 4 16",
+              "light punctual -3 1 5 1 1 1",
+              "mat 1 0.75 0.33 1 1 1 0.8 0 10 0 1", "pl 12 12 -0.5 -12 12 -0.5 -12 -12 -0.5",
+              "mat 1 0.9 0.7 0.5 1 1 1 0.5 30.0827 0 1", "s 0 0 0 0.5"]
+    a, b, c, d, e = "0.272166", "0.643951", "0.172546", "0.371785", "0.0996195"
+    f, z, r = "0.471405", "1.11022e-16", "0.166667"
+    for x, y, zz in ((a, a, "0.544331"), (b, c, z), (c, b, z), ("-" + d, e, "0.544331"), ("-" + f, f, z),
+                     ("-" + b, "-" + c, z), (e, "-" + d, "0.544331"), ("-" + c, "-" + b, z), (f, "-" + f, z)):
+        lines.append(f"s {x} {y} {zz} {r}")
+    return "\n".join(lines) + "\n"

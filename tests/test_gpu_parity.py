@@ -1,0 +1,179 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference goldens.
+
+Bars (north_star): identical traversal decisions (closest-hit object, t and normal bit-equal,
+shadow occlusion equal, identical ray / node / primitive counts), and images within 1e-5 per
+channel of the oracle on identical keyed-RNG seeds.  The only non-bitwise arithmetic is
+powf / expf / double pow (ocml vs glibc, <= 1 ulp), hence the image tolerance.
+"""
+import numpy as np
+import pytest
+
+from tests import scenegen as sg
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5  # per-channel float tolerance (BASELINE.json north_star)
+
+
+@pytest.fixture(scope="module")
+def drt():
+    import distributionraytracer_amd as d
+
+    return d
+
+
+@pytest.fixture(scope="module")
+def renderer(drt):
+    r = drt.Renderer(0)
+    yield r
+    r.close()
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def load_both(drt, O, tmp_path, text, name="s.p3f"):
+    p = sg.write(tmp_path, name, text)
+    return drt.Scene.load_p3f(p), O.Scene.load_p3f(p)
+
+
+def compare_images(img, ref, tol=TOL):
+    assert img.shape == ref.shape
+    assert np.isfinite(img).all() == np.isfinite(ref).all()
+    d = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    d[~np.isfinite(d)] = 0
+    exact = float((img == ref).mean())
+    assert d.max() <= tol, f"max |diff| {d.max():.3g} > {tol} (exact fraction {exact:.4f})"
+    return exact
+
+
+GOLD_CASES = ["tiny", "mixed", "tris2k"]
+
+
+@pytest.mark.parametrize("case", GOLD_CASES)
+def test_bvh_traverse_matches_reference_golden(drt, renderer, tmp_path, case):
+    from tests.test_oracle_pinning import GOLD
+
+    g = np.load(GOLD / f"ref_{case}.npz")
+    p = tmp_path / "s.p3f"
+    p.write_bytes(g["scene_text"].tobytes())
+    s = drt.Scene.load_p3f(p)
+    s.set_accel("bvh")
+    renderer.upload(s)
+    t, n, obj = renderer.trace_closest(g["rays"])
+    np.testing.assert_array_equal(obj, g["bvh_obj"])
+    np.testing.assert_array_equal(bits(t), bits(g["bvh_t"]))
+    np.testing.assert_array_equal(bits(n), bits(g["bvh_n"]))
+    np.testing.assert_array_equal(renderer.trace_shadow(g["shadow_rays"]), g["bvh_occ"])
+
+
+@pytest.mark.parametrize("case", ["mixed", "tris2k"])
+def test_grid_traverse_matches_reference_golden(drt, renderer, tmp_path, case):
+    from tests.test_oracle_pinning import GOLD
+
+    g = np.load(GOLD / f"ref_{case}.npz")
+    p = tmp_path / "s.p3f"
+    p.write_bytes(g["scene_text"].tobytes())
+    s = drt.Scene.load_p3f(p)
+    s.set_accel("grid")
+    renderer.upload(s)
+    t, n, obj = renderer.trace_closest(g["grid_rays"])
+    np.testing.assert_array_equal(obj, g["grid_obj"])
+    np.testing.assert_array_equal(bits(t), bits(g["grid_t"]))
+    np.testing.assert_array_equal(bits(n), bits(g["grid_n"]))
+    np.testing.assert_array_equal(renderer.trace_shadow(g["grid_rays"]), g["grid_occ"])
+
+
+def test_none_traverse_matches_oracle(drt, oracle_mod, renderer, tmp_path):
+    a, b = load_both(drt, oracle_mod, tmp_path, sg.mixed_scene_text(n_tris=200, accel="none"))
+    renderer.upload(a)
+    rays = sg.random_rays(3000, seed=9)
+    t, n, obj = renderer.trace_closest(rays)
+    rt, rn, ro = b.trace_closest(rays)
+    np.testing.assert_array_equal(obj, ro)
+    np.testing.assert_array_equal(bits(t), bits(rt))
+    np.testing.assert_array_equal(bits(n), bits(rn))
+    np.testing.assert_array_equal(renderer.trace_shadow(rays), b.trace_shadow(rays))
+
+
+RENDER_CASES = {
+    # name: (scene text, render kwargs)
+    "aa_bvh_glass_quad": (lambda: sg.mixed_scene_text(res=(40, 32), spp=4, accel="bvh"), {}),
+    "aa_grid_glass_quad": (lambda: sg.mixed_scene_text(res=(40, 32), spp=4, accel="grid"), {}),
+    "aa_none_glass_quad": (lambda: sg.mixed_scene_text(res=(40, 32), spp=4, accel="none", n_tris=40), {}),
+    "aa_nonsquare_spp": (lambda: sg.mixed_scene_text(res=(24, 24), spp=5, accel="bvh"), {}),
+    "whitted_quad_bvh": (lambda: sg.mixed_scene_text(res=(40, 32), spp=0, accel="bvh"), {}),
+    "whitted_point_grid": (lambda: sg.mixed_scene_text(res=(40, 32), spp=0, accel="grid", quad=False), {}),
+    "dof_bvh": (lambda: sg.mixed_scene_text(res=(32, 24), spp=4, accel="bvh", aperture=8.0, focal=1.5), {}),
+    "dof_none": (lambda: sg.mixed_scene_text(res=(32, 24), spp=4, accel="none", n_tris=30, aperture=8.0,
+                                             focal=1.5), {}),
+    "glossy_ext": (lambda: sg.mixed_scene_text(res=(24, 24), spp=4, accel="bvh"), {"roughness": 0.1}),
+    "depth8_ext": (lambda: sg.mixed_scene_text(res=(24, 24), spp=4, accel="bvh"), {"max_depth": 8}),
+    "tris_soup_bvh": (lambda: sg.synthetic_scene_text(20000, res=(48, 48), spp=4), {}),
+    "edge_image_not_multiple_of_tile": (lambda: sg.mixed_scene_text(res=(37, 19), spp=1, accel="bvh"), {}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(RENDER_CASES))
+def test_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
+    mk, kw = RENDER_CASES[case]
+    a, b = load_both(drt, oracle_mod, tmp_path, mk())
+    renderer.upload(a)
+    seed = 12345
+    img = renderer.render(seed=seed, stats=True, **kw)
+    st = renderer.stats()
+    ref, rst = b.render(seed=seed, **kw)
+    compare_images(img, ref)
+    # identical branching => identical traversal work
+    if a.info().accel != 0:
+        assert st["closest_rays"] == rst["closest_calls"]
+        assert st["shadow_rays"] == rst["shadow_calls"]
+    if a.info().accel == 2:
+        assert st["closest_inner"] == rst["closest_inner"] and st["closest_leaf"] == rst["closest_leaf"]
+        assert st["shadow_inner"] == rst["shadow_inner"] and st["shadow_leaf"] == rst["shadow_leaf"]
+        assert st["closest_prims"] == rst["closest_prims"] and st["shadow_prims"] == rst["shadow_prims"]
+    assert st["samples"] == rst["samples"]
+
+
+def test_sharded_frame_equals_whole_frame(drt, renderer, tmp_path):
+    """Interleaved 16x16 tile shards rendered separately and reassembled == one-shot frame."""
+    import torch
+
+    p = sg.write(tmp_path, "s.p3f", sg.mixed_scene_text(res=(70, 45), spp=4, accel="bvh"))
+    s = drt.Scene.load_p3f(p)
+    renderer.upload(s)
+    whole = renderer.render(seed=7)
+    for n_shards in (2, 3, 8):
+        p0 = renderer.frame_params(seed=7, shard=0, n_shards=n_shards)
+        _, floats = renderer.shard_layout(p0)
+        bufs = torch.zeros((n_shards, floats), dtype=torch.float32, device="cuda")
+        for r in range(n_shards):
+            renderer.render_device(renderer.frame_params(seed=7, shard=r, n_shards=n_shards), bufs[r].data_ptr())
+        frame = torch.zeros(whole.shape, dtype=torch.float32, device="cuda")
+        renderer.unshard_device(p0, bufs.data_ptr(), frame.data_ptr())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(frame.cpu().numpy().view(np.uint32), whole.view(np.uint32))
+
+
+def test_reference_scene_balls_low_bvh(drt, oracle_mod, renderer, tmp_path):
+    """SURVEY §8d config 2 geometry (balls_low with accel bvh, 16 spp) at reduced resolution."""
+    text = sg.balls_low_text(res=(96, 96), spp=16, accel="bvh")
+    a, b = load_both(drt, oracle_mod, tmp_path, text)
+    renderer.upload(a)
+    img = renderer.render(seed=99)
+    ref, _ = b.render(seed=99)
+    compare_images(img, ref)
+
+
+def test_full_size_frame_properties(drt, renderer, tmp_path):
+    """At a production size: deterministic re-render, finite, colours clamped to [0, 1]."""
+    p = sg.write(tmp_path, "s.p3f", sg.synthetic_scene_text(100_000, res=(256, 256), spp=16))
+    s = drt.Scene.load_p3f(p)
+    renderer.upload(s)
+    a = renderer.render(seed=3)
+    b = renderer.render(seed=3)
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.isfinite(a).all() and a.min() >= 0.0 and a.max() <= 1.0
+    c = renderer.render(seed=4)
+    assert (a != c).any()
