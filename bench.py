@@ -155,7 +155,7 @@ def main():
     torch.cuda.synchronize()
     st = r.stats()
     keys = ["closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_prims", "shadow_prims",
-            "closest_leaf", "shadow_leaf", "samples"]
+            "closest_leaf", "shadow_leaf", "samples", "wave_node_iters", "wave_path_iters", "lane_path_iters"]
     mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     tot = mine.clone()
     if world > 1:
@@ -225,6 +225,10 @@ def main():
         "node_visits_per_ray": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
                                       tot["shadow_leaf"]) / max(1.0, rays_frame), 2),
         "setup_s": round(build_s, 2),
+        # fraction of lanes doing useful work in the node loop / in the path loop (wave64)
+        "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
+                                         tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3),
+                     "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

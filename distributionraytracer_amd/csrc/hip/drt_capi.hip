@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -16,6 +17,8 @@ void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_onl
 void launch_reduce(const ReduceArgs& A, hipStream_t st);
 void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, int n_tiles, int n_shards,
                     int tiles_per_shard, int res_x, int res_y, hipStream_t st);
+bool persistent_supported(int accel, int mode);
+void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, bool tri_only, bool stats, hipStream_t st);
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
                   float* nrm, int32_t* obj, uint8_t* occ, hipStream_t st);
 }  // namespace drt
@@ -80,7 +83,7 @@ struct drt_ctx {
   float gmin[3] = {0}, gmax[3] = {0};
   DevBuf d_cell_start, d_cell_objs;
   // frame scratch
-  DevBuf d_samples, d_frame, d_stats, d_rays, d_out;
+  DevBuf d_samples, d_frame, d_stats, d_rays, d_out, d_counter;
   drt_frame_stats last{};
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
 };
@@ -98,6 +101,11 @@ struct drt_ctx {
     if (_e != hipSuccess) DRT_FAIL(ctx, _e == hipErrorOutOfMemory ? DRT_E_OOM : DRT_E_HIP, "%s: %s", \
                                    #expr, hipGetErrorString(_e));                                     \
   } while (0)
+
+static int env_int(const char* name, int dflt) {  // tuning knobs for A/B runs
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
 
 static PrimRecord pack_prim(const drt_prim& p, uint32_t mat, uint32_t obj) {
   PrimRecord r{};
@@ -440,7 +448,19 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
   c->frames++;
   DRT_HIP(c, hipEventRecord(ev[0], st));
-  if (P.F.n_items) launch_path(S, P.F, c->accel, c->tri_only, stats, st);
+  const bool persistent = persistent_supported(c->accel, P.F.mode) && env_int("DRT_PERSISTENT", 1) != 0;
+  if (persistent) {
+    DRT_HIP(c, c->d_counter.ensure(256));
+    DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 256, st));
+    P.F.work_counter = c->d_counter.as<unsigned int>();
+    P.F.refill_min = env_int("DRT_REFILL_MIN", 16);
+    P.F.process_min = env_int("DRT_PROCESS_MIN", 16);
+    P.F.waves = env_int("DRT_WAVES", 4);
+  }
+  if (P.F.n_items) {
+    if (persistent) launch_path_persistent(S, P.F, c->tri_only, stats, st);
+    else launch_path(S, P.F, c->accel, c->tri_only, stats, st);
+  }
   DRT_HIP(c, hipGetLastError());
   DRT_HIP(c, hipEventRecord(ev[1], st));
   if (P.F.n_my_tiles) launch_reduce(P.R, st);
@@ -534,6 +554,9 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.shadow_inner = s[ST_S_INNER]; c->last.shadow_leaf = s[ST_S_LEAF];
       c->last.closest_prims = s[ST_C_PRIMS]; c->last.shadow_prims = s[ST_S_PRIMS];
       c->last.samples = s[ST_SAMPLES];
+      c->last.wave_node_iters = s[ST_WAVE_NODE_ITERS];
+      c->last.wave_path_iters = s[ST_WAVE_PATH_ITERS];
+      c->last.lane_path_iters = s[ST_LANE_PATH_ITERS];
     }
   }
   *out = c->last;

@@ -125,6 +125,24 @@ __device__ __forceinline__ bool box_hit(float mnx, float mny, float mnz, float m
   t = (t0 < 0.0f) ? t1 : t0;
   return (t0 < t1) && (t1 > 0.0f);
 }
+// Same test for rays whose three (float)(1.0/d) are finite.  Then no slab product can be NaN
+// ((x - o) is finite, inv finite), and for NaN-free operands MAX3/MIN3's ternary chains and
+// v_max3_f32 / v_min3_f32 select the same value (they may differ only in the sign of a zero
+// result, which no later comparison or selection can observe), so the result is identical.
+__device__ __forceinline__ bool box_hit_finite(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                               const RayP& r, float& t) {
+  const float ax = (mnx - r.o.x) * r.ix, bx = (mxx - r.o.x) * r.ix;
+  const float ay = (mny - r.o.y) * r.iy, by = (mxy - r.o.y) * r.iy;
+  const float az = (mnz - r.o.z) * r.iz, bz = (mxz - r.o.z) * r.iz;
+  const float t0 = fmaxf(fmaxf(r.sx ? ax : bx, r.sy ? ay : by), r.sz ? az : bz);
+  const float t1 = fminf(fminf(r.sx ? bx : ax, r.sy ? by : ay), r.sz ? bz : az);
+  t = (t0 < 0.0f) ? t1 : t0;
+  return (t0 < t1) && (t1 > 0.0f);
+}
+__device__ __forceinline__ bool inv_finite(const RayP& r) {
+  return fabsf(r.ix) < __builtin_inff() && fabsf(r.iy) < __builtin_inff() && fabsf(r.iz) < __builtin_inff();
+}
+
 __device__ __forceinline__ bool box_inside(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, V3 p) {
   return ((p.x > mnx && p.x < mxx) && (p.y > mny && p.y < mxy) && (p.z > mnz && p.z < mxz));
 }

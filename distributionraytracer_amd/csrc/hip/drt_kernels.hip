@@ -9,6 +9,8 @@
 //  * reduce_kernel: ordered per-pixel sum (Color +=, main.cpp:664) and scale (main.cpp:666).
 //  * trace_kernel: batched BVH/Grid/NONE closest and shadow queries (the Traverse() API).
 //  * unshard_kernel: tile-compact shard buffers -> full frame.
+#include <algorithm>
+
 #include "drt_device.hpp"
 #include "drt_kernels.hpp"
 
@@ -24,20 +26,34 @@ struct Counters {
 // first, any hit with t <= range (double len + EPSILON, pre-rounded to a float threshold)
 // ends the query, pops are unconditional.
 // ------------------------------------------------------------------------------------------
+// Traversal stack: the top kLdsStack entries of each thread live in LDS (lane-interleaved:
+// entry k of thread t at [k][t], so a wave's pushes/pops hit 64 consecutive banks); deeper
+// entries spill to a private (scratch) array.  The 1M-triangle SAH tree is 25 levels deep and
+// its stacks rarely exceed ~12 live entries, so the spill path is cold.
+struct TravStack {
+  uint32_t* desc;  // LDS, stride kBlock
+  float* t;        // LDS, stride kBlock
+};
+
+__device__ __forceinline__ bool wave_leader() {
+  return (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__ballot(1));
+}
+
 template <bool TRI_ONLY, bool STATS>
 __device__ __forceinline__ bool bvh_traverse(const SceneArgs& S, const RayP& r, bool shadow, float shadow_thr,
-                                             float& best_t, uint32_t& best_prim, Counters& C) {
+                                             float& best_t, uint32_t& best_prim, Counters& C, TravStack ls) {
   float tmp;
   if (!box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], r, tmp))
     return false;
-  uint32_t st_desc[kMaxBvhDepth];
-  float st_t[kMaxBvhDepth];
+  uint32_t ov_desc[kMaxBvhDepth - kLdsStack];
+  float ov_t[kMaxBvhDepth - kLdsStack];
   int sp = 0;
   uint32_t cur = S.root_desc;
   best_t = 3.402823466e+38f;  // HitRecord t = FLT_MAX
   bool hit = false;
   const float4* __restrict__ nodes = S.nodes;
   while (true) {
+    if (STATS && wave_leader()) C.v[ST_WAVE_NODE_ITERS]++;
     if (!desc_is_leaf(cur)) {
       if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
       const float4* nd = nodes + 4 * (size_t)cur;
@@ -49,10 +65,17 @@ __device__ __forceinline__ bool bvh_traverse(const SceneArgs& S, const RayP& r, 
       if (box_inside(a.x, a.y, a.z, a.w, b.x, b.y, r.o)) tL = 0.0f;
       if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, r.o)) tR = 0.0f;
       if (hL && hR) {
-        bool left_first = shadow ? (tL <= tR) : (tL < tR);
+        const bool left_first = shadow ? (tL <= tR) : (tL < tR);
         cur = left_first ? d.x : d.y;
-        st_desc[sp] = left_first ? d.y : d.x;
-        st_t[sp] = left_first ? tR : tL;
+        const uint32_t pd = left_first ? d.y : d.x;
+        const float pt = left_first ? tR : tL;
+        if (sp < kLdsStack) {
+          ls.desc[sp * kBlock] = pd;
+          ls.t[sp * kBlock] = pt;
+        } else {
+          ov_desc[sp - kLdsStack] = pd;
+          ov_t[sp - kLdsStack] = pt;
+        }
         sp++;
         continue;
       }
@@ -83,8 +106,17 @@ __device__ __forceinline__ bool bvh_traverse(const SceneArgs& S, const RayP& r, 
     bool found = false;
     while (sp > 0) {
       sp--;
-      if (shadow || st_t[sp] < best_t) {
-        cur = st_desc[sp];
+      uint32_t pd;
+      float pt;
+      if (sp < kLdsStack) {
+        pd = ls.desc[sp * kBlock];
+        pt = ls.t[sp * kBlock];
+      } else {
+        pd = ov_desc[sp - kLdsStack];
+        pt = ov_t[sp - kLdsStack];
+      }
+      if (shadow || pt < best_t) {
+        cur = pd;
         found = true;
         break;
       }
@@ -203,9 +235,9 @@ __device__ __forceinline__ bool none_traverse(const SceneArgs& S, const RayP& r,
 
 template <int ACCEL, bool TRI_ONLY, bool STATS>
 __device__ __forceinline__ bool traverse(const SceneArgs& S, const RayP& r, bool shadow, float thr, uint32_t skip,
-                                         float& t, uint32_t& prim, Counters& C) {
+                                         float& t, uint32_t& prim, Counters& C, TravStack ls) {
   if (STATS) C.v[shadow ? ST_SHADOW : ST_CLOSEST]++;
-  if (ACCEL == ACC_BVH) return bvh_traverse<TRI_ONLY, STATS>(S, r, shadow, thr, t, prim, C);
+  if (ACCEL == ACC_BVH) return bvh_traverse<TRI_ONLY, STATS>(S, r, shadow, thr, t, prim, C, ls);
   if (ACCEL == ACC_GRID) return grid_traverse<TRI_ONLY, STATS>(S, r, shadow, thr, t, prim, C);
   return none_traverse<TRI_ONLY, STATS>(S, r, shadow, thr, skip, t, prim, C);
 }
@@ -276,7 +308,8 @@ struct Frame {
 // rayTracing(ray, 1, 1.0, lightSample) — main.cpp:294-521 — as an explicit DFS.
 // ------------------------------------------------------------------------------------------
 template <int ACCEL, bool TRI_ONLY, bool STATS, bool RNG>
-__device__ V3 trace_path(const SceneArgs& S, const FrameArgs& F, RayP q, V3 ls, KRng& rng, Counters& C) {
+__device__ V3 trace_path(const SceneArgs& S, const FrameArgs& F, RayP q, V3 ls, KRng& rng, Counters& C,
+                         TravStack tst) {
   Frame fr[kMaxFrames];
   int sp = 0;
   int depth = 1;
@@ -292,9 +325,13 @@ __device__ V3 trace_path(const SceneArgs& S, const FrameArgs& F, RayP q, V3 ls, 
   V3 result = mk(0, 0, 0);
 
   while (true) {
+    if (STATS) {
+      C.v[ST_LANE_PATH_ITERS]++;
+      if (wave_leader()) C.v[ST_WAVE_PATH_ITERS]++;
+    }
     float t = 0.f;
     uint32_t prim = 0;
-    const bool hit = traverse<ACCEL, TRI_ONLY, STATS>(S, q, shadow, thr, hitPrim, t, prim, C);
+    const bool hit = traverse<ACCEL, TRI_ONLY, STATS>(S, q, shadow, thr, hitPrim, t, prim, C, tst);
 
     bool ret = false;  // the current node produced its return value `c`
     V3 c = mk(0, 0, 0);
@@ -509,26 +546,28 @@ __device__ __forceinline__ void flush_stats(const FrameArgs& F, const Counters& 
   }
 }
 
-template <int ACCEL, bool TRI_ONLY, bool STATS>
-__global__ void __launch_bounds__(256) path_kernel(SceneArgs S, FrameArgs F) {
+template <int ACCEL, bool TRI_ONLY, bool STATS, int MODE>
+__global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
+  TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + kLdsStack * kBlock) + threadIdx.x};
   const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counters C;
   for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
   if (item < F.n_items) {
-    const int per_pixel = (F.mode == MODE_SEQ) ? 1 : F.nsub;
+    const int per_pixel = (MODE == MODE_SEQ) ? 1 : F.nsub;
     Item it = decode_item(F, S.res_x, S.res_y, item, per_pixel);
     V3 color = mk(0, 0, 0);
     if (it.valid) {
       const uint32_t P = (uint32_t)(it.y * S.res_x + it.x);
       const uint32_t pmix = P * 0x9E3779B9u;
       KRng rng{F.seed, pmix, 0};
-      if (F.mode == MODE_AA) {
+      if (MODE == MODE_AA) {
         float rx, ry, sx, sy;
         sample_prologue(F, pmix, it.sub, rx, ry, sx, sy);
         RayP r = primary_ray(S, (float)it.x + rx, (float)it.y + ry);
         if (STATS) C.v[ST_SAMPLES]++;
-        color = trace_path<ACCEL, TRI_ONLY, STATS, false>(S, F, r, mk(sx, sy, 0.0f), rng, C);
-      } else if (F.mode == MODE_SEQ) {
+        color = trace_path<ACCEL, TRI_ONLY, STATS, false>(S, F, r, mk(sx, sy, 0.0f), rng, C, tst);
+      } else if (MODE == MODE_SEQ) {
         if (F.spp > 0) {  // AA with DoF and/or glossy reflection: the keyed stream in call order
           rng.k = 5u * F.spp - 1u;
           for (int p = 0; p < (int)F.spp; p++) {
@@ -539,8 +578,7 @@ __global__ void __launch_bounds__(256) path_kernel(SceneArgs S, FrameArgs F) {
             if (F.dof) r = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
             else r = primary_ray(S, px, py);
             if (STATS) C.v[ST_SAMPLES]++;
-            V3 c = trace_path<ACCEL, TRI_ONLY, STATS, true>(S, F, r, mk(sx, sy, 0.0f), rng, C);
-            color = add(color, c);
+            color = add(color, trace_path<ACCEL, TRI_ONLY, STATS, true>(S, F, r, mk(sx, sy, 0.0f), rng, C, tst));
           }
         } else {  // Whitted with glossy reflection: each light sample in order on one stream
           RayP r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
@@ -550,23 +588,406 @@ __global__ void __launch_bounds__(256) path_kernel(SceneArgs S, FrameArgs F) {
                                     ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
                                : mk(0.5f, 0.5f, 0.0f);
             if (STATS) C.v[ST_SAMPLES]++;
-            color = add(color, trace_path<ACCEL, TRI_ONLY, STATS, true>(S, F, r, ls, rng, C));
+            color = add(color, trace_path<ACCEL, TRI_ONLY, STATS, true>(S, F, r, ls, rng, C, tst));
           }
         }
-      } else if (F.mode == MODE_WHITTED_QUAD) {
+      } else if (MODE == MODE_WHITTED_QUAD) {
         const int s = it.sub;
         V3 ls = mk(((float)(s % F.grid_size) + 0.5f) / (float)F.grid_size,
                    ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f);
         RayP r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
         if (STATS) C.v[ST_SAMPLES]++;
-        color = trace_path<ACCEL, TRI_ONLY, STATS, false>(S, F, r, ls, rng, C);
+        color = trace_path<ACCEL, TRI_ONLY, STATS, false>(S, F, r, ls, rng, C, tst);
       } else {
         RayP r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
         if (STATS) C.v[ST_SAMPLES]++;
-        color = trace_path<ACCEL, TRI_ONLY, STATS, false>(S, F, r, mk(0.5f, 0.5f, 0.0f), rng, C);
+        color = trace_path<ACCEL, TRI_ONLY, STATS, false>(S, F, r, mk(0.5f, 0.5f, 0.0f), rng, C, tst);
       }
     }
     F.samples[item] = make_float4(color.x, color.y, color.z, 0.0f);
+  }
+  flush_stats<STATS>(F, C);
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent BVH path kernel (modes without RNG in the path: AA, Whitted quad/point).
+//
+// Each lane runs rayTracing()'s DFS as an explicit state machine and every loop iteration
+// does ONE unit of work per lane: a BVH node step (inner node, or leaf + stack pops) for lanes
+// with a query in flight, or a shading step (consume a query result, set up the next shadow /
+// secondary query or unwind a finished frame) for lanes whose query has completed.  Shading is
+// batched: it runs only when `process_min` lanes are waiting (or nobody is traversing), so the
+// long shading code is not re-entered for a single lane.  Lanes whose sample is finished are
+// refilled from a global work counter, `refill_min` at a time, so waves never drain while any
+// work is left.  Results are per work item (sample) exactly as in path_kernel; the ordered
+// per-pixel reduce is unchanged, so frames are bit-identical.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kNoItem = 0xFFFFFFFFu;
+
+struct Lane {
+  uint32_t item;
+  // query in flight
+  RayP q;
+  uint32_t cur, best_prim;
+  int sp;
+  float best_t, thr;
+  bool shadow, in_trav, hit, pop, finite;
+  // path (rayTracing call chain)
+  int depth, fsp;
+  float ior1;
+  V3 ls;
+  // node being shaded
+  V3 hitP, N, V, acc, lightPos;
+  float NdotL, NdotH, hitT;
+  uint32_t hitPrim, mat;
+  bool outside;
+  int j;
+};
+
+template <bool STATS>
+__device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const RayP& q, bool shadow, float thr,
+                                            Counters& C) {
+  if (STATS) C.v[shadow ? ST_SHADOW : ST_CLOSEST]++;
+  L.q = q;
+  L.shadow = shadow;
+  L.thr = thr;
+  L.sp = 0;
+  L.best_t = 3.402823466e+38f;
+  L.hit = false;
+  L.cur = S.root_desc;
+  L.pop = false;
+  L.finite = inv_finite(q);
+  float tmp;
+  L.in_trav = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], q,
+                      tmp);  // bvh.cpp:242 / :328: a root miss is an immediate (empty) result
+}
+
+// One iteration of the node loop of bvh.cpp:245-312 / :331-388: visit node `cur` (both child
+// boxes of an inner node, or every primitive of a leaf), then — if the visit produced no next
+// node — make ONE pop attempt.  A closest-hit pop that is pruned (t >= best, bvh.cpp:303) leaves
+// `pop` set, so the next iteration tries the next entry; the visit order is exactly the
+// reference's, only spread over iterations with uniform, short control flow.
+template <bool TRI_ONLY, bool STATS>
+__device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, TravStack ls, uint32_t* ov_desc,
+                                          float* ov_t, bool wave_finite, Counters& C) {
+  if (!L.pop) {
+    const uint32_t cur = L.cur;
+    if (!desc_is_leaf(cur)) {
+      if (STATS) C.v[L.shadow ? ST_S_INNER : ST_C_INNER]++;
+      const float4* nd = S.nodes + 4 * (size_t)cur;
+      const float4 a = nd[0], b = nd[1], c = nd[2];
+      const uint4 d = *reinterpret_cast<const uint4*>(nd + 3);
+      float tL, tR;
+      bool hL, hR;
+      if (wave_finite) {
+        hL = box_hit_finite(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
+        hR = box_hit_finite(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
+      } else {
+        hL = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
+        hR = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
+      }
+      if (box_inside(a.x, a.y, a.z, a.w, b.x, b.y, L.q.o)) tL = 0.0f;
+      if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, L.q.o)) tR = 0.0f;
+      const bool both = hL && hR;
+      const bool left_first = L.shadow ? (tL <= tR) : (tL < tR);
+      L.cur = both ? (left_first ? d.x : d.y) : (hL ? d.x : d.y);
+      L.pop = !(hL || hR);
+      if (both) {
+        const uint32_t pd = left_first ? d.y : d.x;
+        const float pt = left_first ? tR : tL;
+        const int sp = L.sp;
+        if (sp < kLdsStack) {
+          ls.desc[sp * kBlock] = pd;
+          ls.t[sp * kBlock] = pt;
+        } else {
+          ov_desc[sp - kLdsStack] = pd;
+          ov_t[sp - kLdsStack] = pt;
+        }
+        L.sp = sp + 1;
+      }
+    } else {
+      if (STATS) C.v[L.shadow ? ST_S_LEAF : ST_C_LEAF]++;
+      uint32_t first = desc_first(cur), cnt = desc_count(cur);
+      if (cnt == kBigLeaf) {
+        const uint2 bl = S.big_leaves[first];
+        first = bl.x;
+        cnt = bl.y;
+      }
+      for (uint32_t i = 0; i < cnt; i++) {
+        if (STATS) C.v[L.shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+        float t;
+        if (hit_prim<TRI_ONLY>(S.prims, first + i, L.q, t)) {
+          if (L.shadow) {
+            if (t <= L.thr) {
+              L.hit = true;
+              L.in_trav = false;  // any-hit: done (bvh.cpp:376-377)
+              return;
+            }
+          } else if (t < L.best_t) {
+            L.best_t = t;
+            L.best_prim = first + i;
+            L.hit = true;
+          }
+        }
+      }
+      L.pop = true;
+    }
+  }
+  if (L.pop) {  // bvh.cpp:299-311 / :381-387
+    if (L.sp == 0) {
+      L.in_trav = false;
+    } else {
+      const int sp = --L.sp;
+      uint32_t pd;
+      float pt;
+      if (sp < kLdsStack) {
+        pd = ls.desc[sp * kBlock];
+        pt = ls.t[sp * kBlock];
+      } else {
+        pd = ov_desc[sp - kLdsStack];
+        pt = ov_t[sp - kLdsStack];
+      }
+      if (L.shadow || pt < L.best_t) {
+        L.cur = pd;
+        L.pop = false;
+      }
+    }
+  }
+}
+
+template <bool STATS>
+__device__ __forceinline__ void setup_shadow(const SceneArgs& S, Lane& L, Counters& C) {  // main.cpp:386-422
+  const drt_light& Lt = S.lights[L.j];
+  if (Lt.type == DRT_LIGHT_QUAD) L.lightPos = add(add(ld3(Lt.pos), mul(ld3(Lt.e1), L.ls.x)), mul(ld3(Lt.e2), L.ls.y));
+  else L.lightPos = ld3(Lt.pos);
+  V3 Lv = sub(L.lightPos, L.hitP);
+  const V3 Ls = Lv;
+  Lv = normalize(Lv);
+  const V3 H = normalize(add(Lv, L.V));
+  L.NdotL = smax(dot(L.N, Lv), 0.0f);
+  L.NdotH = smax(dot(L.N, H), 0.0f);
+  // BVH::Traverse(Ray&) normalises Ls and accepts t <= |Ls| + EPSILON (bvh.cpp:321-322, :376)
+  start_query<STATS>(S, L, make_ray(add(L.hitP, mul(L.N, 1e-4f)), normalize(Ls)), true, shadow_threshold(length(Ls)),
+                     C);
+}
+
+// Consume the completed query of lane L (main.cpp:294-521 between two traversals).
+template <bool STATS>
+__device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Frame* fr, Counters& C) {
+  const float offset = 1e-4f;
+  V3 c = mk(0, 0, 0);
+  bool ret = false;
+  bool after_lights = false;
+  if (!L.shadow) {
+    if (!L.hit) {  // main.cpp:351-357
+      c = cclamp(background(S, L.q.d));
+      ret = true;
+    } else {
+      L.hitT = L.best_t;
+      L.hitPrim = L.best_prim;
+      L.hitP = add(L.q.o, mul(L.q.d, L.hitT));
+      L.N = normalize(prim_normal(S.prims, L.hitPrim, L.q, L.hitT));
+      L.outside = dot(L.q.d, L.N) < 0.0f;
+      if (!L.outside) L.N = neg(L.N);
+      L.mat = prim_material(S.prims[3 * L.hitPrim]);
+      L.V = neg(normalize(L.q.d));
+      L.acc = mk(0, 0, 0);
+      L.lightPos = mk(0, 0, 0);
+      L.j = 0;
+      if (S.n_lights > 0) {
+        setup_shadow<STATS>(S, L, C);
+        return;
+      }
+      after_lights = true;
+    }
+  } else {  // main.cpp:444-450
+    if (!L.hit) {
+      const drt_material& m = S.mats[L.mat];
+      const V3 diff = mul(mul(ld3(m.diff), m.kd), L.NdotL);
+      const V3 spec = mul(mul(ld3(m.spec), m.ks), powf(L.NdotH, m.shine));
+      L.acc = add(L.acc, add(diff, spec));
+    }
+    L.j++;
+    if (L.j < S.n_lights) {
+      setup_shadow<STATS>(S, L, C);
+      return;
+    }
+    after_lights = true;
+  }
+  if (after_lights) {  // main.cpp:453-520
+    const drt_material& m = S.mats[L.mat];
+    if (L.depth > F.max_depth) {
+      c = L.acc;
+      ret = true;
+    } else {
+      float kr = m.refl;
+      float ior2 = m.ior;
+      if (!L.outside) ior2 = 1.0f;
+      const float eta = L.ior1 / ior2;
+      const V3 Vt = sub(mul(L.N, dot(L.V, L.N)), L.V);
+      const float sin_i = length(Vt);
+      const V3 tv = dvf(Vt, length(Vt));
+      const float sin_t = eta * sin_i;
+      const bool has_refr = (m.trans == 1.0f && sin_t < 1.0f);
+      const bool has_refl = m.ks > 0.0f;
+      V3 beer = mk(1.f, 1.f, 1.f);
+      RayP child = L.q;
+      float child_ior = L.ior1;
+      if (has_refr) {
+        const float sin_t2 = (float)((double)sin_t * (double)sin_t);
+        const float cos_t = sqrtf(1.0f - sin_t2);
+        const V3 r_t = normalize(add(mul(tv, sin_t), mul(neg(L.N), cos_t)));
+        const float cos_i = dot(L.N, L.V);
+        const float cosTheta = (L.ior1 > ior2) ? cos_t : cos_i;
+        float r0 = (L.ior1 - ior2) / (L.ior1 + ior2);
+        r0 = (float)((double)r0 * (double)r0);
+        kr = (float)((double)r0 + (double)(1.0f - r0) * pow((double)(1.0f - cosTheta), 5.0));
+        if (!L.outside) {
+          const V3 e = mul(sub(mk(1.f, 1.f, 1.f), ld3(m.diff)), -L.hitT);
+          beer = mk(expf(e.x), expf(e.y), expf(e.z));
+        }
+        child = make_ray(sub(L.hitP, mul(L.N, offset)), r_t);
+        child_ior = ior2;
+      } else if (m.trans > 0.0f && sin_t >= 1.0f) {
+        kr = 1.0f;
+      }
+      if (has_refr || has_refl) {
+        Frame& f = fr[L.fsp++];
+        f.acc = L.acc; f.hitP = L.hitP; f.N = L.N; f.V = L.V; f.lightPos = L.lightPos; f.beer = beer;
+        f.ior1 = L.ior1; f.kr = kr; f.mat = L.mat;
+        f.flags = (has_refr ? 0u : 1u) | (L.outside ? 2u : 0u) | (has_refl ? 4u : 0u);
+        if (!has_refr) {
+          const V3 R = normalize(sub(mul(mul(L.N, dot(L.V, L.N)), 2.0f), L.V));
+          if (dot(R, L.N) > 0.0f) f.flags |= 8u;
+          child = make_ray(add(L.hitP, mul(L.N, offset)), R);
+          child_ior = L.ior1;
+        }
+        L.ior1 = child_ior;
+        L.ls = L.lightPos;
+        L.depth++;
+        start_query<STATS>(S, L, child, false, 0.0f, C);
+        return;
+      }
+      c = cclamp(L.acc);
+      ret = true;
+    }
+  }
+  // unwind: c is the return value of the current rayTracing() call
+  while (L.fsp > 0) {
+    Frame& f = fr[L.fsp - 1];
+    if ((f.flags & 1u) == 0u) {
+      V3 rc = cclamp(c);
+      if ((f.flags & 2u) == 0u) rc = cmulc(rc, f.beer);
+      f.acc = add(f.acc, mul(rc, 1.0f - f.kr));
+      if (f.flags & 4u) {
+        f.flags |= 1u;
+        const V3 R = normalize(sub(mul(mul(f.N, dot(f.V, f.N)), 2.0f), f.V));
+        if (dot(R, f.N) > 0.0f) f.flags |= 8u;
+        L.ior1 = f.ior1;
+        L.ls = f.lightPos;
+        L.depth = L.fsp + 1;
+        start_query<STATS>(S, L, make_ray(add(f.hitP, mul(f.N, offset)), R), false, 0.0f, C);
+        return;
+      }
+      c = cclamp(f.acc);
+      L.fsp--;
+    } else {
+      const V3 rc = cclamp(c);
+      if (f.flags & 8u) f.acc = add(f.acc, cmulc(mul(rc, f.kr), ld3(S.mats[f.mat].spec)));
+      c = cclamp(f.acc);
+      L.fsp--;
+    }
+  }
+  (void)ret;
+  F.samples[L.item] = make_float4(c.x, c.y, c.z, 0.0f);  // rayTracing(depth = 1) returned
+  L.item = kNoItem;
+}
+
+template <bool STATS, int MODE>
+__device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item,
+                                          Counters& C) {
+  L.item = item;
+  const int per_pixel = F.nsub;
+  const Item it = decode_item(F, S.res_x, S.res_y, item, per_pixel);
+  if (!it.valid) {  // padding of a partial tile
+    F.samples[item] = make_float4(0.f, 0.f, 0.f, 0.f);
+    L.item = kNoItem;
+    return;
+  }
+  L.depth = 1;
+  L.fsp = 0;
+  L.ior1 = 1.0f;
+  if (STATS) C.v[ST_SAMPLES]++;
+  RayP r;
+  if (MODE == MODE_AA) {
+    const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+    float rx, ry, sx, sy;
+    sample_prologue(F, pmix, it.sub, rx, ry, sx, sy);
+    r = primary_ray(S, (float)it.x + rx, (float)it.y + ry);
+    L.ls = mk(sx, sy, 0.0f);
+  } else if (MODE == MODE_WHITTED_QUAD) {
+    const int s = it.sub;
+    L.ls = mk(((float)(s % F.grid_size) + 0.5f) / (float)F.grid_size,
+              ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f);
+    r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
+  } else {
+    L.ls = mk(0.5f, 0.5f, 0.0f);
+    r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
+  }
+  start_query<STATS>(S, L, r, false, 0.0f, C);
+}
+
+template <bool TRI_ONLY, bool STATS, int MODE, int WAVES>
+__global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, FrameArgs F) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
+  const TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + kLdsStack * kBlock) + threadIdx.x};
+  uint32_t ov_desc[kMaxBvhDepth - kLdsStack];
+  float ov_t[kMaxBvhDepth - kLdsStack];
+  Frame fr[kMaxFrames];
+  Counters C;
+  for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
+  Lane L;
+  L.item = kNoItem;
+  L.in_trav = false;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t n_items = (uint32_t)F.n_items;
+  bool exhausted = false;  // wave-uniform
+  while (true) {
+    // ---- refill idle lanes from the global work counter (one atomic per wave)
+    const uint64_t idle = __ballot(L.item == kNoItem);
+    const int n_idle = __popcll(idle);
+    if (!exhausted && (n_idle >= F.refill_min || n_idle == 64)) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(F.work_counter, (unsigned)n_idle);
+      base = __shfl(base, 0, 64);
+      if (base + (uint32_t)n_idle >= n_items) exhausted = true;
+      if (L.item == kNoItem) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        const uint32_t it = base + rank;
+        if (it < n_items) lane_init<STATS, MODE>(S, F, L, it, C);
+      }
+    }
+    const bool live = L.item != kNoItem;
+    const uint64_t trav = __ballot(live && L.in_trav);
+    const uint64_t ready = __ballot(live && !L.in_trav);
+    if (trav == 0 && ready == 0) {
+      if (exhausted) break;
+      continue;
+    }
+    // ---- one node step for every lane with a query in flight
+    if (trav) {
+      if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
+      const bool wave_finite = __ballot(live && L.in_trav && !L.finite) == 0;
+      if (live && L.in_trav) node_step<TRI_ONLY, STATS>(S, L, tst, ov_desc, ov_t, wave_finite, C);
+    }
+    // ---- batched shading for lanes whose query completed
+    if (ready && (__popcll(ready) >= F.process_min || trav == 0 || exhausted)) {
+      if (STATS) {
+        if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
+        if (live && !L.in_trav) C.v[ST_LANE_PATH_ITERS]++;
+      }
+      if (live && !L.in_trav) lane_process<STATS>(S, F, L, fr, C);
+    }
   }
   flush_stats<STATS>(F, C);
 }
@@ -615,8 +1036,10 @@ __global__ void __launch_bounds__(256) unshard_kernel(const float* __restrict__ 
 
 // Batched Traverse() queries.
 template <int ACCEL, bool TRI_ONLY>
-__global__ void __launch_bounds__(256) trace_kernel(SceneArgs S, const float* __restrict__ rays, int n, int shadow,
-                                                    float* t_out, float* n_out, int32_t* obj_out, uint8_t* occ_out) {
+__global__ void __launch_bounds__(kBlock) trace_kernel(SceneArgs S, const float* __restrict__ rays, int n, int shadow,
+                                                       float* t_out, float* n_out, int32_t* obj_out, uint8_t* occ_out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
+  TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + kLdsStack * kBlock) + threadIdx.x};
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* rr = rays + 6 * (size_t)i;
@@ -626,7 +1049,7 @@ __global__ void __launch_bounds__(256) trace_kernel(SceneArgs S, const float* __
   uint32_t prim = 0;
   if (!shadow) {
     RayP r = make_ray(o, d);
-    bool hit = traverse<ACCEL, TRI_ONLY, false>(S, r, false, 0.f, 0xFFFFFFFFu, t, prim, C);
+    bool hit = traverse<ACCEL, TRI_ONLY, false>(S, r, false, 0.f, 0xFFFFFFFFu, t, prim, C, tst);
     if (hit) {
       V3 nn = prim_normal(S.prims, prim, r, t);
       t_out[i] = t;
@@ -644,18 +1067,68 @@ __global__ void __launch_bounds__(256) trace_kernel(SceneArgs S, const float* __
     if (ACCEL == ACC_BVH) { thr = shadow_threshold(len); r = make_ray(o, normalize(d)); }
     else if (ACCEL == ACC_GRID) { thr = len; r = make_ray(o, normalize(d)); }
     else { thr = len; r = make_ray(o, d); }
-    occ_out[i] = traverse<ACCEL, TRI_ONLY, false>(S, r, true, thr, 0xFFFFFFFFu, t, prim, C) ? 1 : 0;
+    occ_out[i] = traverse<ACCEL, TRI_ONLY, false>(S, r, true, thr, 0xFFFFFFFFu, t, prim, C, tst) ? 1 : 0;
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // Host-side launchers (C++ linkage, called from drt_capi.hip)
 // ------------------------------------------------------------------------------------------
+constexpr size_t kStackLds = (size_t)kLdsStack * kBlock * 8;  // desc + t per entry
+
+template <int A, bool T, int M>
+static void launch_path_m(const SceneArgs& S, const FrameArgs& F, bool stats, hipStream_t st) {
+  const uint64_t blocks = (F.n_items + kBlock - 1) / kBlock;
+  if (stats) hipLaunchKernelGGL((path_kernel<A, T, true, M>), dim3((unsigned)blocks), dim3(kBlock), kStackLds, st, S, F);
+  else hipLaunchKernelGGL((path_kernel<A, T, false, M>), dim3((unsigned)blocks), dim3(kBlock), kStackLds, st, S, F);
+}
 template <int A, bool T>
 static void launch_path_t(const SceneArgs& S, const FrameArgs& F, bool stats, hipStream_t st) {
-  const uint64_t blocks = (F.n_items + 255) / 256;
-  if (stats) hipLaunchKernelGGL((path_kernel<A, T, true>), dim3((unsigned)blocks), dim3(256), 0, st, S, F);
-  else hipLaunchKernelGGL((path_kernel<A, T, false>), dim3((unsigned)blocks), dim3(256), 0, st, S, F);
+  switch (F.mode) {
+    case MODE_AA: launch_path_m<A, T, MODE_AA>(S, F, stats, st); break;
+    case MODE_SEQ: launch_path_m<A, T, MODE_SEQ>(S, F, stats, st); break;
+    case MODE_WHITTED_QUAD: launch_path_m<A, T, MODE_WHITTED_QUAD>(S, F, stats, st); break;
+    default: launch_path_m<A, T, MODE_WHITTED_POINT>(S, F, stats, st); break;
+  }
+}
+
+template <bool T, bool ST, int M, int W>
+static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
+  static int grid = 0;  // resident blocks across the device (per instantiation)
+  if (!grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_persistent<T, ST, M, W>, kBlock,
+                                                       kStackLds);
+    grid = std::max(1, cus) * std::max(1, per_cu);
+  }
+  const uint64_t need = (F.n_items + kBlock - 1) / kBlock;
+  const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);
+  hipLaunchKernelGGL((path_persistent<T, ST, M, W>), dim3(blocks), dim3(kBlock), kStackLds, st, S, F);
+}
+template <bool T, bool ST, int M>
+static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
+  switch (F.waves) {  // register budget: waves per SIMD the kernel is compiled for
+    case 2: launch_persistent_w<T, ST, M, 2>(S, F, st); break;
+    case 3: launch_persistent_w<T, ST, M, 3>(S, F, st); break;
+    default: launch_persistent_w<T, ST, M, 4>(S, F, st); break;
+  }
+}
+template <bool T, bool ST>
+static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
+  switch (F.mode) {
+    case MODE_AA: launch_persistent_m<T, ST, MODE_AA>(S, F, st); break;
+    case MODE_WHITTED_QUAD: launch_persistent_m<T, ST, MODE_WHITTED_QUAD>(S, F, st); break;
+    default: launch_persistent_m<T, ST, MODE_WHITTED_POINT>(S, F, st); break;
+  }
+}
+
+bool persistent_supported(int accel, int mode) { return accel == ACC_BVH && mode != MODE_SEQ; }
+
+void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, bool tri_only, bool stats, hipStream_t st) {
+  if (tri_only) { if (stats) launch_persistent_t<true, true>(S, F, st); else launch_persistent_t<true, false>(S, F, st); }
+  else { if (stats) launch_persistent_t<false, true>(S, F, st); else launch_persistent_t<false, false>(S, F, st); }
 }
 
 void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats, hipStream_t st) {
@@ -678,8 +1151,8 @@ void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, in
 
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
                   float* nrm, int32_t* obj, uint8_t* occ, hipStream_t st) {
-  dim3 g((n + 255) / 256), b(256);
-#define DRT_TRACE(A, T) hipLaunchKernelGGL((trace_kernel<A, T>), g, b, 0, st, S, rays, n, shadow, t, nrm, obj, occ)
+  dim3 g((n + kBlock - 1) / kBlock), b(kBlock);
+#define DRT_TRACE(A, T) hipLaunchKernelGGL((trace_kernel<A, T>), g, b, kStackLds, st, S, rays, n, shadow, t, nrm, obj, occ)
   if (accel == ACC_BVH) { if (tri_only) DRT_TRACE(ACC_BVH, true); else DRT_TRACE(ACC_BVH, false); }
   else if (accel == ACC_GRID) { if (tri_only) DRT_TRACE(ACC_GRID, true); else DRT_TRACE(ACC_GRID, false); }
   else { if (tri_only) DRT_TRACE(ACC_NONE, true); else DRT_TRACE(ACC_NONE, false); }

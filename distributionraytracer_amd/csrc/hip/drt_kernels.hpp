@@ -18,11 +18,16 @@ enum FrameMode : int {
 
 enum StatSlot : int {
   ST_CLOSEST = 0, ST_SHADOW, ST_C_INNER, ST_C_LEAF, ST_S_INNER, ST_S_LEAF, ST_C_PRIMS, ST_S_PRIMS, ST_SAMPLES,
+  // SIMD efficiency: wave-level iterations of the node loop / of the path loop (one count per
+  // wave per iteration, by its lowest active lane)
+  ST_WAVE_NODE_ITERS, ST_WAVE_PATH_ITERS, ST_LANE_PATH_ITERS,
   ST_COUNT
 };
 
 constexpr int kMaxFrames = 16;     // max_depth <= 15
 constexpr int kMaxBvhDepth = 96;   // traversal stack entries (host rejects deeper trees)
+constexpr int kLdsStack = 16;      // traversal stack entries kept in LDS per thread
+constexpr int kBlock = 256;        // path-kernel block size
 
 struct SceneArgs {
   // Camera (camera.h:32-61), precomputed on the host
@@ -66,6 +71,10 @@ struct FrameArgs {
   uint64_t n_items;
   float4* samples;
   unsigned long long* stats;
+  unsigned int* work_counter;  // persistent kernel: next unclaimed work item (zeroed per frame)
+  int refill_min;              // persistent kernel: refill a wave once this many lanes are idle
+  int process_min;             // persistent kernel: shade once this many lanes have a result
+  int waves;                   // persistent kernel: register budget (waves per SIMD: 2, 3 or 4)
 };
 
 struct ReduceArgs {

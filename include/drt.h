@@ -142,6 +142,8 @@ typedef struct {
   uint64_t samples;                       /* rayTracing(depth = 1) calls                 */
   double render_ms;                        /* device time of the last drt_render*        */
   double kernel_ms;                        /* device time of the path-tracing kernel     */
+  uint64_t wave_node_iters;                /* node-loop iterations counted once per wave */
+  uint64_t wave_path_iters, lane_path_iters; /* path-loop iterations per wave / per lane  */
 } drt_frame_stats;
 
 int drt_create(drt_ctx** out, const drt_options* opt);
