@@ -155,7 +155,8 @@ def main():
     torch.cuda.synchronize()
     st = r.stats()
     keys = ["closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_prims", "shadow_prims",
-            "closest_leaf", "shadow_leaf", "samples", "wave_node_iters", "wave_path_iters", "lane_path_iters"]
+            "closest_leaf", "shadow_leaf", "samples", "wave_node_iters", "wave_path_iters", "lane_path_iters",
+            "cycles_refill", "cycles_node", "cycles_shade"]
     mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     tot = mine.clone()
     if world > 1:
@@ -229,6 +230,10 @@ def main():
         "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
                                          tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3),
                      "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3)},
+        # share of the persistent kernel's wave cycles per loop section (stats frame)
+        "cycle_share": {k: round(tot["cycles_" + k] / max(1.0, tot["cycles_refill"] + tot["cycles_node"] +
+                                                           tot["cycles_shade"]), 3)
+                        for k in ("refill", "node", "shade")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

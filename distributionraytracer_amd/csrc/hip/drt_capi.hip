@@ -453,9 +453,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DRT_HIP(c, c->d_counter.ensure(256));
     DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 256, st));
     P.F.work_counter = c->d_counter.as<unsigned int>();
-    P.F.refill_min = env_int("DRT_REFILL_MIN", 16);
+    P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
     P.F.process_min = env_int("DRT_PROCESS_MIN", 16);
-    P.F.waves = env_int("DRT_WAVES", 4);
+    P.F.waves = env_int("DRT_WAVES", 6);
   }
   if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->tri_only, stats, st);
@@ -557,6 +557,9 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.wave_node_iters = s[ST_WAVE_NODE_ITERS];
       c->last.wave_path_iters = s[ST_WAVE_PATH_ITERS];
       c->last.lane_path_iters = s[ST_LANE_PATH_ITERS];
+      c->last.cycles_refill = s[ST_CYC_REFILL];
+      c->last.cycles_node = s[ST_CYC_NODE];
+      c->last.cycles_shade = s[ST_CYC_PROC];
     }
   }
   *out = c->last;

@@ -100,13 +100,16 @@ __device__ __forceinline__ V3 rnd_unit_sphere(KRng& g) {
 struct RayP {
   V3 o, d;
   float ix, iy, iz;   // (float)(1.0 / d)
-  bool sx, sy, sz;    // inv >= 0  (false for NaN)
+  // slab sign selectors (boundingBox.cpp:69-101: inv >= 0, false for NaN), recomputed on use so
+  // they are never carried as lane masks across loops
+  __device__ __forceinline__ bool sx() const { return ix >= 0.0f; }
+  __device__ __forceinline__ bool sy() const { return iy >= 0.0f; }
+  __device__ __forceinline__ bool sz() const { return iz >= 0.0f; }
 };
 __device__ __forceinline__ RayP make_ray(V3 o, V3 d) {
   RayP r;
   r.o = o; r.d = d;
   r.ix = 1.0f / d.x; r.iy = 1.0f / d.y; r.iz = 1.0f / d.z;
-  r.sx = r.ix >= 0.0f; r.sy = r.iy >= 0.0f; r.sz = r.iz >= 0.0f;
   return r;
 }
 
@@ -114,12 +117,12 @@ __device__ __forceinline__ RayP make_ray(V3 o, V3 d) {
 // caller's "if inside: t = 0" (bvh.cpp:256-257).
 __device__ __forceinline__ bool box_hit(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
                                         const RayP& r, float& t) {
-  float txmin = ((r.sx ? mnx : mxx) - r.o.x) * r.ix;
-  float txmax = ((r.sx ? mxx : mnx) - r.o.x) * r.ix;
-  float tymin = ((r.sy ? mny : mxy) - r.o.y) * r.iy;
-  float tymax = ((r.sy ? mxy : mny) - r.o.y) * r.iy;
-  float tzmin = ((r.sz ? mnz : mxz) - r.o.z) * r.iz;
-  float tzmax = ((r.sz ? mxz : mnz) - r.o.z) * r.iz;
+  float txmin = ((r.sx() ? mnx : mxx) - r.o.x) * r.ix;
+  float txmax = ((r.sx() ? mxx : mnx) - r.o.x) * r.ix;
+  float tymin = ((r.sy() ? mny : mxy) - r.o.y) * r.iy;
+  float tymax = ((r.sy() ? mxy : mny) - r.o.y) * r.iy;
+  float tzmin = ((r.sz() ? mnz : mxz) - r.o.z) * r.iz;
+  float tzmax = ((r.sz() ? mxz : mnz) - r.o.z) * r.iz;
   float t0 = max3(txmin, tymin, tzmin);
   float t1 = min3(txmax, tymax, tzmax);
   t = (t0 < 0.0f) ? t1 : t0;
@@ -134,8 +137,8 @@ __device__ __forceinline__ bool box_hit_finite(float mnx, float mny, float mnz, 
   const float ax = (mnx - r.o.x) * r.ix, bx = (mxx - r.o.x) * r.ix;
   const float ay = (mny - r.o.y) * r.iy, by = (mxy - r.o.y) * r.iy;
   const float az = (mnz - r.o.z) * r.iz, bz = (mxz - r.o.z) * r.iz;
-  const float t0 = fmaxf(fmaxf(r.sx ? ax : bx, r.sy ? ay : by), r.sz ? az : bz);
-  const float t1 = fminf(fminf(r.sx ? bx : ax, r.sy ? by : ay), r.sz ? bz : az);
+  const float t0 = fmaxf(fmaxf(r.sx() ? ax : bx, r.sy() ? ay : by), r.sz() ? az : bz);
+  const float t1 = fminf(fminf(r.sx() ? bx : ax, r.sy() ? by : ay), r.sz() ? bz : az);
   t = (t0 < 0.0f) ? t1 : t0;
   return (t0 < t1) && (t1 > 0.0f);
 }

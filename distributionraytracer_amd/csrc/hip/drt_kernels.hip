@@ -142,9 +142,9 @@ __device__ bool grid_traverse(const SceneArgs& S, const RayP& r, bool shadow, fl
   const float x0 = S.gmin[0], y0 = S.gmin[1], z0 = S.gmin[2], x1 = S.gmax[0], y1 = S.gmax[1], z1 = S.gmax[2];
   const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
   float txmin, tymin, tzmin, txmax, tymax, tzmax;
-  if (r.sx) { txmin = (x0 - ox) * r.ix; txmax = (x1 - ox) * r.ix; } else { txmin = (x1 - ox) * r.ix; txmax = (x0 - ox) * r.ix; }
-  if (r.sy) { tymin = (y0 - oy) * r.iy; tymax = (y1 - oy) * r.iy; } else { tymin = (y1 - oy) * r.iy; tymax = (y0 - oy) * r.iy; }
-  if (r.sz) { tzmin = (z0 - oz) * r.iz; tzmax = (z1 - oz) * r.iz; } else { tzmin = (z1 - oz) * r.iz; tzmax = (z0 - oz) * r.iz; }
+  if (r.sx()) { txmin = (x0 - ox) * r.ix; txmax = (x1 - ox) * r.ix; } else { txmin = (x1 - ox) * r.ix; txmax = (x0 - ox) * r.ix; }
+  if (r.sy()) { tymin = (y0 - oy) * r.iy; tymax = (y1 - oy) * r.iy; } else { tymin = (y1 - oy) * r.iy; tymax = (y0 - oy) * r.iy; }
+  if (r.sz()) { tzmin = (z0 - oz) * r.iz; tzmax = (z1 - oz) * r.iz; } else { tzmin = (z1 - oz) * r.iz; tzmax = (z0 - oz) * r.iz; }
   float t0 = (txmin > tymin) ? txmin : tymin;
   if (tzmin > t0) t0 = tzmin;
   float t1 = (txmax < tymax) ? txmax : tymax;
@@ -624,14 +624,31 @@ __global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) 
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;
 
+// LDS traversal-stack entries per thread for a given occupancy target (5 blocks of 256 threads
+// fit 16 entries in 160 KiB; 6-8 blocks need a shorter LDS stack, the rest spills to scratch).
+__host__ __device__ constexpr int lds_cap(int waves) {
+  return (160 * 1024 / (waves * kBlock * 8) - 1) < 16 ? (160 * 1024 / (waves * kBlock * 8) - 1) : 16;
+}
+
+// Per-lane state flags, packed into one VGPR: divergent bools kept as separate variables
+// become 64-bit SGPR lane masks that the loop has to carry (and spill) across iterations.
+enum LaneFlag : uint32_t {
+  LF_SHADOW = 1u,   // query in flight is a shadow (any-hit) query
+  LF_TRAV = 2u,     // query still traversing
+  LF_HIT = 4u,      // query found a hit
+  LF_POP = 8u,      // next node step starts with a pop attempt
+  LF_FINITE = 16u,  // ray origin and (float)(1.0/d) are all finite
+  LF_OUTSIDE = 32u  // shading state: the hit was on the outside of the surface (main.cpp:364)
+};
+
 struct Lane {
   uint32_t item;
+  uint32_t fl;  // LaneFlag bits
   // query in flight
   RayP q;
   uint32_t cur, best_prim;
   int sp;
   float best_t, thr;
-  bool shadow, in_trav, hit, pop, finite;
   // path (rayTracing call chain)
   int depth, fsp;
   float ior1;
@@ -640,73 +657,96 @@ struct Lane {
   V3 hitP, N, V, acc, lightPos;
   float NdotL, NdotH, hitT;
   uint32_t hitPrim, mat;
-  bool outside;
   int j;
 };
+
+// AABB::hit + isInside (boundingBox.cpp:41-44, :64-124; bvh.cpp:256-257) for a ray whose origin
+// and slab constants are finite.  Every slab product is then finite and, because a child box has
+// min <= max, the product from the near plane is the smaller one on every axis: min/max pick
+// exactly the values the reference's sign-selected MAX3/MIN3 pick (a zero may differ in sign,
+// which no later comparison can observe).  `p > mn` equals `mn - p < 0` for finite floats (a
+// difference of distinct floats never rounds to zero), so the inside test reuses the slab
+// differences.
+__device__ __forceinline__ bool box_test_finite(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                                const RayP& r, float& t) {
+  const float dnx = mnx - r.o.x, dny = mny - r.o.y, dnz = mnz - r.o.z;
+  const float dxx = mxx - r.o.x, dxy = mxy - r.o.y, dxz = mxz - r.o.z;
+  const float ax = dnx * r.ix, bx = dxx * r.ix;
+  const float ay = dny * r.iy, by = dxy * r.iy;
+  const float az = dnz * r.iz, bz = dxz * r.iz;
+  const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+  const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+  const bool inside = (fmaxf(fmaxf(dnx, dny), dnz) < 0.0f) && (fminf(fminf(dxx, dxy), dxz) > 0.0f);
+  t = inside ? 0.0f : ((t0 < 0.0f) ? t1 : t0);
+  return (t0 < t1) && (t1 > 0.0f);
+}
+__device__ __forceinline__ bool ray_finite(const RayP& r) {
+  return inv_finite(r) && fabsf(r.o.x) < __builtin_inff() && fabsf(r.o.y) < __builtin_inff() &&
+         fabsf(r.o.z) < __builtin_inff();
+}
 
 template <bool STATS>
 __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const RayP& q, bool shadow, float thr,
                                             Counters& C) {
   if (STATS) C.v[shadow ? ST_SHADOW : ST_CLOSEST]++;
   L.q = q;
-  L.shadow = shadow;
   L.thr = thr;
   L.sp = 0;
   L.best_t = 3.402823466e+38f;
-  L.hit = false;
   L.cur = S.root_desc;
-  L.pop = false;
-  L.finite = inv_finite(q);
   float tmp;
-  L.in_trav = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4], S.root_box[5], q,
-                      tmp);  // bvh.cpp:242 / :328: a root miss is an immediate (empty) result
+  const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
+                            S.root_box[5], q, tmp);  // bvh.cpp:242 / :328: a root miss is an empty result
+  L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (ray_finite(q) ? LF_FINITE : 0u);
 }
 
 // One iteration of the node loop of bvh.cpp:245-312 / :331-388: visit node `cur` (both child
 // boxes of an inner node, or every primitive of a leaf), then — if the visit produced no next
 // node — make ONE pop attempt.  A closest-hit pop that is pruned (t >= best, bvh.cpp:303) leaves
-// `pop` set, so the next iteration tries the next entry; the visit order is exactly the
+// LF_POP set, so the next iteration tries the next entry; the visit order is exactly the
 // reference's, only spread over iterations with uniform, short control flow.
-template <bool TRI_ONLY, bool STATS>
+template <bool TRI_ONLY, bool STATS, int CAP>
 __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, TravStack ls, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C) {
-  if (!L.pop) {
+  uint32_t fl = L.fl;
+  const bool shadow = (fl & LF_SHADOW) != 0u;
+  if (!(fl & LF_POP)) {
     const uint32_t cur = L.cur;
     if (!desc_is_leaf(cur)) {
-      if (STATS) C.v[L.shadow ? ST_S_INNER : ST_C_INNER]++;
+      if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
       const float4* nd = S.nodes + 4 * (size_t)cur;
       const float4 a = nd[0], b = nd[1], c = nd[2];
       const uint4 d = *reinterpret_cast<const uint4*>(nd + 3);
       float tL, tR;
       bool hL, hR;
       if (wave_finite) {
-        hL = box_hit_finite(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
-        hR = box_hit_finite(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
+        hL = box_test_finite(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
+        hR = box_test_finite(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
       } else {
         hL = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
         hR = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
+        if (box_inside(a.x, a.y, a.z, a.w, b.x, b.y, L.q.o)) tL = 0.0f;
+        if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, L.q.o)) tR = 0.0f;
       }
-      if (box_inside(a.x, a.y, a.z, a.w, b.x, b.y, L.q.o)) tL = 0.0f;
-      if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, L.q.o)) tR = 0.0f;
       const bool both = hL && hR;
-      const bool left_first = L.shadow ? (tL <= tR) : (tL < tR);
-      L.cur = both ? (left_first ? d.x : d.y) : (hL ? d.x : d.y);
-      L.pop = !(hL || hR);
-      if (both) {
-        const uint32_t pd = left_first ? d.y : d.x;
-        const float pt = left_first ? tR : tL;
-        const int sp = L.sp;
-        if (sp < kLdsStack) {
-          ls.desc[sp * kBlock] = pd;
-          ls.t[sp * kBlock] = pt;
-        } else {
-          ov_desc[sp - kLdsStack] = pd;
-          ov_t[sp - kLdsStack] = pt;
-        }
-        L.sp = sp + 1;
+      const bool left_first = shadow ? (tL <= tR) : (tL < tR);
+      L.cur = (hL && (left_first || !hR)) ? d.x : d.y;
+      fl |= (hL | hR) ? 0u : LF_POP;
+      // push the far child (bvh.cpp:268-283); the LDS slot above the top is free, so the store
+      // is unconditional and only the stack pointer depends on `both`
+      const uint32_t pd = left_first ? d.y : d.x;
+      const float pt = left_first ? tR : tL;
+      const int sp = L.sp;
+      if (sp < CAP) {
+        ls.desc[sp * kBlock] = pd;
+        ls.t[sp * kBlock] = pt;
+      } else if (both) {
+        ov_desc[sp - CAP] = pd;
+        ov_t[sp - CAP] = pt;
       }
+      L.sp = sp + (both ? 1 : 0);
     } else {
-      if (STATS) C.v[L.shadow ? ST_S_LEAF : ST_C_LEAF]++;
+      if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
       uint32_t first = desc_first(cur), cnt = desc_count(cur);
       if (cnt == kBigLeaf) {
         const uint2 bl = S.big_leaves[first];
@@ -714,45 +754,45 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, TravStack
         cnt = bl.y;
       }
       for (uint32_t i = 0; i < cnt; i++) {
-        if (STATS) C.v[L.shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+        if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
         float t;
         if (hit_prim<TRI_ONLY>(S.prims, first + i, L.q, t)) {
-          if (L.shadow) {
-            if (t <= L.thr) {
-              L.hit = true;
-              L.in_trav = false;  // any-hit: done (bvh.cpp:376-377)
+          if (shadow) {
+            if (t <= L.thr) {  // any-hit: done (bvh.cpp:376-377)
+              L.fl = (fl | LF_HIT) & ~LF_TRAV;
               return;
             }
           } else if (t < L.best_t) {
             L.best_t = t;
             L.best_prim = first + i;
-            L.hit = true;
+            fl |= LF_HIT;
           }
         }
       }
-      L.pop = true;
+      fl |= LF_POP;
     }
   }
-  if (L.pop) {  // bvh.cpp:299-311 / :381-387
+  if (fl & LF_POP) {  // bvh.cpp:299-311 / :381-387
     if (L.sp == 0) {
-      L.in_trav = false;
+      fl &= ~LF_TRAV;
     } else {
       const int sp = --L.sp;
       uint32_t pd;
       float pt;
-      if (sp < kLdsStack) {
+      if (sp < CAP) {
         pd = ls.desc[sp * kBlock];
         pt = ls.t[sp * kBlock];
       } else {
-        pd = ov_desc[sp - kLdsStack];
-        pt = ov_t[sp - kLdsStack];
+        pd = ov_desc[sp - CAP];
+        pt = ov_t[sp - CAP];
       }
-      if (L.shadow || pt < L.best_t) {
+      if (shadow || pt < L.best_t) {
         L.cur = pd;
-        L.pop = false;
+        fl &= ~LF_POP;
       }
     }
   }
+  L.fl = fl;
 }
 
 template <bool STATS>
@@ -776,19 +816,19 @@ template <bool STATS>
 __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Frame* fr, Counters& C) {
   const float offset = 1e-4f;
   V3 c = mk(0, 0, 0);
-  bool ret = false;
   bool after_lights = false;
-  if (!L.shadow) {
-    if (!L.hit) {  // main.cpp:351-357
+  const bool hit = (L.fl & LF_HIT) != 0u;
+  if (!(L.fl & LF_SHADOW)) {
+    if (!hit) {  // main.cpp:351-357
       c = cclamp(background(S, L.q.d));
-      ret = true;
     } else {
       L.hitT = L.best_t;
       L.hitPrim = L.best_prim;
       L.hitP = add(L.q.o, mul(L.q.d, L.hitT));
       L.N = normalize(prim_normal(S.prims, L.hitPrim, L.q, L.hitT));
-      L.outside = dot(L.q.d, L.N) < 0.0f;
-      if (!L.outside) L.N = neg(L.N);
+      const bool outside = dot(L.q.d, L.N) < 0.0f;
+      if (!outside) L.N = neg(L.N);
+      L.fl = outside ? (L.fl | LF_OUTSIDE) : (L.fl & ~LF_OUTSIDE);
       L.mat = prim_material(S.prims[3 * L.hitPrim]);
       L.V = neg(normalize(L.q.d));
       L.acc = mk(0, 0, 0);
@@ -801,7 +841,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       after_lights = true;
     }
   } else {  // main.cpp:444-450
-    if (!L.hit) {
+    if (!hit) {
       const drt_material& m = S.mats[L.mat];
       const V3 diff = mul(mul(ld3(m.diff), m.kd), L.NdotL);
       const V3 spec = mul(mul(ld3(m.spec), m.ks), powf(L.NdotH, m.shine));
@@ -816,13 +856,13 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
   }
   if (after_lights) {  // main.cpp:453-520
     const drt_material& m = S.mats[L.mat];
+    const bool outside = (L.fl & LF_OUTSIDE) != 0u;
     if (L.depth > F.max_depth) {
       c = L.acc;
-      ret = true;
     } else {
       float kr = m.refl;
       float ior2 = m.ior;
-      if (!L.outside) ior2 = 1.0f;
+      if (!outside) ior2 = 1.0f;
       const float eta = L.ior1 / ior2;
       const V3 Vt = sub(mul(L.N, dot(L.V, L.N)), L.V);
       const float sin_i = length(Vt);
@@ -842,7 +882,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         float r0 = (L.ior1 - ior2) / (L.ior1 + ior2);
         r0 = (float)((double)r0 * (double)r0);
         kr = (float)((double)r0 + (double)(1.0f - r0) * pow((double)(1.0f - cosTheta), 5.0));
-        if (!L.outside) {
+        if (!outside) {
           const V3 e = mul(sub(mk(1.f, 1.f, 1.f), ld3(m.diff)), -L.hitT);
           beer = mk(expf(e.x), expf(e.y), expf(e.z));
         }
@@ -855,7 +895,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         Frame& f = fr[L.fsp++];
         f.acc = L.acc; f.hitP = L.hitP; f.N = L.N; f.V = L.V; f.lightPos = L.lightPos; f.beer = beer;
         f.ior1 = L.ior1; f.kr = kr; f.mat = L.mat;
-        f.flags = (has_refr ? 0u : 1u) | (L.outside ? 2u : 0u) | (has_refl ? 4u : 0u);
+        f.flags = (has_refr ? 0u : 1u) | (outside ? 2u : 0u) | (has_refl ? 4u : 0u);
         if (!has_refr) {
           const V3 R = normalize(sub(mul(mul(L.N, dot(L.V, L.N)), 2.0f), L.V));
           if (dot(R, L.N) > 0.0f) f.flags |= 8u;
@@ -869,7 +909,6 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         return;
       }
       c = cclamp(L.acc);
-      ret = true;
     }
   }
   // unwind: c is the return value of the current rayTracing() call
@@ -898,7 +937,6 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       L.fsp--;
     }
   }
-  (void)ret;
   F.samples[L.item] = make_float4(c.x, c.y, c.z, 0.0f);  // rayTracing(depth = 1) returned
   L.item = kNoItem;
 }
@@ -917,6 +955,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
   L.depth = 1;
   L.fsp = 0;
   L.ior1 = 1.0f;
+  L.fl = 0u;
   if (STATS) C.v[ST_SAMPLES]++;
   RayP r;
   if (MODE == MODE_AA) {
@@ -939,20 +978,30 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
 
 template <bool TRI_ONLY, bool STATS, int MODE, int WAVES>
 __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, FrameArgs F) {
+  constexpr int CAP = lds_cap(WAVES);
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
-  const TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + kLdsStack * kBlock) + threadIdx.x};
-  uint32_t ov_desc[kMaxBvhDepth - kLdsStack];
-  float ov_t[kMaxBvhDepth - kLdsStack];
+  const TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + CAP * kBlock) + threadIdx.x};
+  uint32_t ov_desc[kMaxBvhDepth - CAP];
+  float ov_t[kMaxBvhDepth - CAP];
   Frame fr[kMaxFrames];
   Counters C;
   for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
   Lane L;
   L.item = kNoItem;
-  L.in_trav = false;
+  L.fl = 0u;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_items = (uint32_t)F.n_items;
   bool exhausted = false;  // wave-uniform
+  uint64_t cyc[3] = {0, 0, 0};  // stats builds: refill / node / shading section cycles (wave-uniform)
+  auto stamp = [&]() -> uint64_t {
+    if (!STATS) return 0;
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  };
   while (true) {
+    const uint64_t t0 = stamp();
     // ---- refill idle lanes from the global work counter (one atomic per wave)
     const uint64_t idle = __ballot(L.item == kNoItem);
     const int n_idle = __popcll(idle);
@@ -968,28 +1017,43 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
       }
     }
     const bool live = L.item != kNoItem;
-    const uint64_t trav = __ballot(live && L.in_trav);
-    const uint64_t ready = __ballot(live && !L.in_trav);
+    const bool in_trav = live && (L.fl & LF_TRAV);
+    const uint64_t trav = __ballot(in_trav);
+    const uint64_t ready = __ballot(live && !(L.fl & LF_TRAV));
     if (trav == 0 && ready == 0) {
       if (exhausted) break;
       continue;
     }
+    const uint64_t t1 = stamp();
     // ---- one node step for every lane with a query in flight
     if (trav) {
       if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
-      const bool wave_finite = __ballot(live && L.in_trav && !L.finite) == 0;
-      if (live && L.in_trav) node_step<TRI_ONLY, STATS>(S, L, tst, ov_desc, ov_t, wave_finite, C);
+      const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
+      if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, tst, ov_desc, ov_t, wave_finite, C);
     }
+    const uint64_t t2 = stamp();
     // ---- batched shading for lanes whose query completed
+    const bool done = live && !(L.fl & LF_TRAV);
     if (ready && (__popcll(ready) >= F.process_min || trav == 0 || exhausted)) {
       if (STATS) {
         if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
-        if (live && !L.in_trav) C.v[ST_LANE_PATH_ITERS]++;
+        if (done) C.v[ST_LANE_PATH_ITERS]++;
       }
-      if (live && !L.in_trav) lane_process<STATS>(S, F, L, fr, C);
+      if (done) lane_process<STATS>(S, F, L, fr, C);
+    }
+    if (STATS) {
+      const uint64_t t3 = stamp();
+      cyc[0] += t1 - t0;
+      cyc[1] += t2 - t1;
+      cyc[2] += t3 - t2;
     }
   }
   flush_stats<STATS>(F, C);
+  if (STATS && lane == 0) {
+    atomicAdd(&F.stats[ST_CYC_REFILL], (unsigned long long)cyc[0]);
+    atomicAdd(&F.stats[ST_CYC_NODE], (unsigned long long)cyc[1]);
+    atomicAdd(&F.stats[ST_CYC_PROC], (unsigned long long)cyc[2]);
+  }
 }
 
 // Ordered sum over a pixel's items (Color += in sample order, main.cpp:664 / :694) and scale.
@@ -1100,18 +1164,22 @@ static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStrea
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_persistent<T, ST, M, W>, kBlock,
-                                                       kStackLds);
+                                                       (size_t)lds_cap(W) * kBlock * 8);
     grid = std::max(1, cus) * std::max(1, per_cu);
   }
   const uint64_t need = (F.n_items + kBlock - 1) / kBlock;
   const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);
-  hipLaunchKernelGGL((path_persistent<T, ST, M, W>), dim3(blocks), dim3(kBlock), kStackLds, st, S, F);
+  hipLaunchKernelGGL((path_persistent<T, ST, M, W>), dim3(blocks), dim3(kBlock), (size_t)lds_cap(W) * kBlock * 8, st,
+                     S, F);
 }
 template <bool T, bool ST, int M>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
   switch (F.waves) {  // register budget: waves per SIMD the kernel is compiled for
-    case 2: launch_persistent_w<T, ST, M, 2>(S, F, st); break;
     case 3: launch_persistent_w<T, ST, M, 3>(S, F, st); break;
+    case 5: launch_persistent_w<T, ST, M, 5>(S, F, st); break;
+    case 6: launch_persistent_w<T, ST, M, 6>(S, F, st); break;
+    case 7: launch_persistent_w<T, ST, M, 7>(S, F, st); break;
+    case 8: launch_persistent_w<T, ST, M, 8>(S, F, st); break;
     default: launch_persistent_w<T, ST, M, 4>(S, F, st); break;
   }
 }

@@ -21,6 +21,8 @@ enum StatSlot : int {
   // SIMD efficiency: wave-level iterations of the node loop / of the path loop (one count per
   // wave per iteration, by its lowest active lane)
   ST_WAVE_NODE_ITERS, ST_WAVE_PATH_ITERS, ST_LANE_PATH_ITERS,
+  // stats builds of the persistent kernel: s_memtime cycles per wave in each loop section
+  ST_CYC_REFILL, ST_CYC_NODE, ST_CYC_PROC,
   ST_COUNT
 };
 

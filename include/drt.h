@@ -144,6 +144,7 @@ typedef struct {
   double kernel_ms;                        /* device time of the path-tracing kernel     */
   uint64_t wave_node_iters;                /* node-loop iterations counted once per wave */
   uint64_t wave_path_iters, lane_path_iters; /* path-loop iterations per wave / per lane  */
+  uint64_t cycles_refill, cycles_node, cycles_shade; /* persistent kernel: s_memtime cycles */
 } drt_frame_stats;
 
 int drt_create(drt_ctx** out, const drt_options* opt);

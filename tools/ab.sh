@@ -14,7 +14,7 @@ for v in "$@"; do
   python - "$v" $OUT/ab_$i.json <<'PY'
 import json,sys
 try:
-    d=json.load(open(sys.argv[2])); print(f"{sys.argv[1]:40s} {d['value']:8.1f} Mrays/s {d['ms_per_step']:8.1f} ms  simd={d['simd_eff']}  frac={d['roofline']['frac']}")
+    d=json.load(open(sys.argv[2])); print(f"{sys.argv[1]:40s} {d['value']:8.1f} Mrays/s {d['ms_per_step']:8.1f} ms  simd={d['simd_eff']} cyc={d.get('cycle_share')} frac={d['roofline']['frac']}")
 except Exception as e: print(sys.argv[1], 'FAILED', e)
 PY
   [ $rc -eq 0 ] || exit $rc
