@@ -156,7 +156,7 @@ def main():
     st = r.stats()
     keys = ["closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_prims", "shadow_prims",
             "closest_leaf", "shadow_leaf", "samples", "wave_node_iters", "wave_path_iters", "lane_path_iters",
-            "cycles_refill", "cycles_node", "cycles_shade"]
+            "cycles_refill", "cycles_node", "cycles_shade", "stack_pushes", "stack_spills"]
     mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     tot = mine.clone()
     if world > 1:
@@ -230,6 +230,9 @@ def main():
         "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
                                          tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3),
                      "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3)},
+        # traversal-stack pushes per ray and the share that went past the LDS part (scratch)
+        "stack": {"pushes_per_ray": round(tot["stack_pushes"] / max(1.0, rays_frame), 2),
+                  "spill_frac": round(tot["stack_spills"] / max(1.0, tot["stack_pushes"]), 4)},
         # share of the persistent kernel's wave cycles per loop section (stats frame)
         "cycle_share": {k: round(tot["cycles_" + k] / max(1.0, tot["cycles_refill"] + tot["cycles_node"] +
                                                            tot["cycles_shade"]), 3)

@@ -49,7 +49,7 @@ class DrtFrameStats(C.Structure):
                                           "shadow_inner", "shadow_leaf", "closest_prims", "shadow_prims",
                                           "samples")] + [("render_ms", C.c_double), ("kernel_ms", C.c_double)] + \
         [(n, C.c_uint64) for n in ("wave_node_iters", "wave_path_iters", "lane_path_iters", "cycles_refill",
-                                   "cycles_node", "cycles_shade")]
+                                   "cycles_node", "cycles_shade", "stack_pushes", "stack_spills")]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_}

@@ -454,7 +454,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 256, st));
     P.F.work_counter = c->d_counter.as<unsigned int>();
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
-    P.F.process_min = env_int("DRT_PROCESS_MIN", 16);
+    P.F.process_min = env_int("DRT_PROCESS_MIN", 24);
     P.F.waves = env_int("DRT_WAVES", 6);
   }
   if (P.F.n_items) {
@@ -560,6 +560,8 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.cycles_refill = s[ST_CYC_REFILL];
       c->last.cycles_node = s[ST_CYC_NODE];
       c->last.cycles_shade = s[ST_CYC_PROC];
+      c->last.stack_pushes = s[ST_PUSH];
+      c->last.stack_spills = s[ST_PUSH_SPILL];
     }
   }
   *out = c->last;

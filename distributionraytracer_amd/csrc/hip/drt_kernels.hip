@@ -30,9 +30,15 @@ struct Counters {
 // entry k of thread t at [k][t], so a wave's pushes/pops hit 64 consecutive banks); deeper
 // entries spill to a private (scratch) array.  The 1M-triangle SAH tree is 25 levels deep and
 // its stacks rarely exceed ~12 live entries, so the spill path is cold.
+// LDS-typed pointers: with plain (generic) pointers the compiler merges the LDS and the scratch
+// arms of a pop into one flat_load, which waits on both memory paths.
+typedef __attribute__((address_space(3))) uint8_t LdsByte;
+typedef __attribute__((address_space(3))) uint32_t LdsU32;
+typedef __attribute__((address_space(3))) float LdsF32;
+
 struct TravStack {
-  uint32_t* desc;  // LDS, stride kBlock
-  float* t;        // LDS, stride kBlock
+  LdsU32* desc;  // stride kBlock
+  LdsF32* t;     // stride kBlock
 };
 
 __device__ __forceinline__ bool wave_leader() {
@@ -549,7 +555,7 @@ __device__ __forceinline__ void flush_stats(const FrameArgs& F, const Counters& 
 template <int ACCEL, bool TRI_ONLY, bool STATS, int MODE>
 __global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
-  TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + kLdsStack * kBlock) + threadIdx.x};
+  TravStack tst{(LdsU32*)lds_stack + threadIdx.x, (LdsF32*)(lds_stack + kLdsStack * kBlock) + threadIdx.x};
   const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Counters C;
   for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
@@ -647,7 +653,10 @@ struct Lane {
   // query in flight
   RayP q;
   uint32_t cur, best_prim;
-  int sp;
+  // traversal-stack pointer as an LDS byte address: spa = depth * 1024 + threadIdx.x * 4 (the
+  // [entry][thread] layout of a 256-thread block), so depth = spa >> 10 and the lane's own
+  // column survives in the low bits — no base address has to stay live across the loop
+  uint32_t spa;
   float best_t, thr;
   // path (rayTracing call chain)
   int depth, fsp;
@@ -676,9 +685,12 @@ __device__ __forceinline__ bool box_test_finite(float mnx, float mny, float mnz,
   const float az = dnz * r.iz, bz = dxz * r.iz;
   const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
   const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-  const bool inside = (fmaxf(fmaxf(dnx, dny), dnz) < 0.0f) && (fminf(fminf(dxx, dxy), dxz) > 0.0f);
-  t = inside ? 0.0f : ((t0 < 0.0f) ? t1 : t0);
-  return (t0 < t1) && (t1 > 0.0f);
+  // inside <=> max(mn - o) < 0 && min(mx - o) > 0 <=> max(max(mn - o), -min(mx - o)) < 0, and
+  // hit <=> t0 < t1 && t1 > 0 <=> max(t0, 0) < t1 — both exact without NaNs, and branch-free
+  const float in = fmaxf(fmaxf(fmaxf(dnx, dny), dnz), -fminf(fminf(dxx, dxy), dxz));
+  const float te = (t0 < 0.0f) ? t1 : t0;
+  t = (in < 0.0f) ? 0.0f : te;
+  return fmaxf(t0, 0.0f) < t1;
 }
 __device__ __forceinline__ bool ray_finite(const RayP& r) {
   return inv_finite(r) && fabsf(r.o.x) < __builtin_inff() && fabsf(r.o.y) < __builtin_inff() &&
@@ -691,7 +703,7 @@ __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const R
   if (STATS) C.v[shadow ? ST_SHADOW : ST_CLOSEST]++;
   L.q = q;
   L.thr = thr;
-  L.sp = 0;
+  L.spa &= 1023u;
   L.best_t = 3.402823466e+38f;
   L.cur = S.root_desc;
   float tmp;
@@ -706,8 +718,9 @@ __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const R
 // LF_POP set, so the next iteration tries the next entry; the visit order is exactly the
 // reference's, only spread over iterations with uniform, short control flow.
 template <bool TRI_ONLY, bool STATS, int CAP>
-__device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, TravStack ls, uint32_t* ov_desc,
+__device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C) {
+  constexpr uint32_t kLdsBytes = (uint32_t)CAP * kBlock * 4u;  // desc part; the t part follows
   uint32_t fl = L.fl;
   const bool shadow = (fl & LF_SHADOW) != 0u;
   if (!(fl & LF_POP)) {
@@ -729,22 +742,30 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, TravStack
         if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, L.q.o)) tR = 0.0f;
       }
       const bool both = hL && hR;
-      const bool left_first = shadow ? (tL <= tR) : (tL < tR);
+      // shadow: tL <= tR, closest: tL < tR (bvh.cpp:262 / :344).  Only consulted when both boxes
+      // are hit, and then tL, tR are non-NaN and >= 0 (or -0), so they order as sign-cleared
+      // integers and `<=` is `< + 1`.
+      const uint32_t uL = __float_as_uint(tL) & 0x7fffffffu, uR = __float_as_uint(tR) & 0x7fffffffu;
+      const bool left_first = uL < uR + (fl & LF_SHADOW);
       L.cur = (hL && (left_first || !hR)) ? d.x : d.y;
       fl |= (hL | hR) ? 0u : LF_POP;
       // push the far child (bvh.cpp:268-283); the LDS slot above the top is free, so the store
       // is unconditional and only the stack pointer depends on `both`
       const uint32_t pd = left_first ? d.y : d.x;
       const float pt = left_first ? tR : tL;
-      const int sp = L.sp;
-      if (sp < CAP) {
-        ls.desc[sp * kBlock] = pd;
-        ls.t[sp * kBlock] = pt;
+      const uint32_t spa = L.spa;
+      if (spa < kLdsBytes) {
+        *(LdsU32*)(lds + spa) = pd;
+        *(LdsF32*)(lds + kLdsBytes + spa) = pt;
       } else if (both) {
-        ov_desc[sp - CAP] = pd;
-        ov_t[sp - CAP] = pt;
+        ov_desc[(spa >> 10) - CAP] = pd;
+        ov_t[(spa >> 10) - CAP] = pt;
       }
-      L.sp = sp + (both ? 1 : 0);
+      L.spa = spa + (both ? 1024u : 0u);
+      if (STATS && both) {
+        C.v[ST_PUSH]++;
+        if (spa >= kLdsBytes) C.v[ST_PUSH_SPILL]++;
+      }
     } else {
       if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
       uint32_t first = desc_first(cur), cnt = desc_count(cur);
@@ -773,18 +794,19 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, TravStack
     }
   }
   if (fl & LF_POP) {  // bvh.cpp:299-311 / :381-387
-    if (L.sp == 0) {
+    if (L.spa < 1024u) {
       fl &= ~LF_TRAV;
     } else {
-      const int sp = --L.sp;
+      const uint32_t spa = L.spa - 1024u;
+      L.spa = spa;
       uint32_t pd;
       float pt;
-      if (sp < CAP) {
-        pd = ls.desc[sp * kBlock];
-        pt = ls.t[sp * kBlock];
+      if (spa < kLdsBytes) {
+        pd = *(LdsU32*)(lds + spa);
+        pt = *(LdsF32*)(lds + kLdsBytes + spa);
       } else {
-        pd = ov_desc[sp - CAP];
-        pt = ov_t[sp - CAP];
+        pd = ov_desc[(spa >> 10) - CAP];
+        pt = ov_t[(spa >> 10) - CAP];
       }
       if (shadow || pt < L.best_t) {
         L.cur = pd;
@@ -979,8 +1001,8 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
 template <bool TRI_ONLY, bool STATS, int MODE, int WAVES>
 __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, FrameArgs F) {
   constexpr int CAP = lds_cap(WAVES);
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
-  const TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + CAP * kBlock) + threadIdx.x};
+  static_assert(kBlock * 4 == 1024, "spa encoding assumes 256-thread blocks");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_bytes[];
   uint32_t ov_desc[kMaxBvhDepth - CAP];
   float ov_t[kMaxBvhDepth - CAP];
   Frame fr[kMaxFrames];
@@ -989,6 +1011,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
   Lane L;
   L.item = kNoItem;
   L.fl = 0u;
+  L.spa = threadIdx.x * 4u;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_items = (uint32_t)F.n_items;
   bool exhausted = false;  // wave-uniform
@@ -1029,7 +1052,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
     if (trav) {
       if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
       const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
-      if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, tst, ov_desc, ov_t, wave_finite, C);
+      if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C);
     }
     const uint64_t t2 = stamp();
     // ---- batched shading for lanes whose query completed
@@ -1103,7 +1126,7 @@ template <int ACCEL, bool TRI_ONLY>
 __global__ void __launch_bounds__(kBlock) trace_kernel(SceneArgs S, const float* __restrict__ rays, int n, int shadow,
                                                        float* t_out, float* n_out, int32_t* obj_out, uint8_t* occ_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
-  TravStack tst{lds_stack + threadIdx.x, reinterpret_cast<float*>(lds_stack + kLdsStack * kBlock) + threadIdx.x};
+  TravStack tst{(LdsU32*)lds_stack + threadIdx.x, (LdsF32*)(lds_stack + kLdsStack * kBlock) + threadIdx.x};
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* rr = rays + 6 * (size_t)i;
@@ -1175,12 +1198,10 @@ static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStrea
 template <bool T, bool ST, int M>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
   switch (F.waves) {  // register budget: waves per SIMD the kernel is compiled for
-    case 3: launch_persistent_w<T, ST, M, 3>(S, F, st); break;
     case 5: launch_persistent_w<T, ST, M, 5>(S, F, st); break;
-    case 6: launch_persistent_w<T, ST, M, 6>(S, F, st); break;
     case 7: launch_persistent_w<T, ST, M, 7>(S, F, st); break;
     case 8: launch_persistent_w<T, ST, M, 8>(S, F, st); break;
-    default: launch_persistent_w<T, ST, M, 4>(S, F, st); break;
+    default: launch_persistent_w<T, ST, M, 6>(S, F, st); break;
   }
 }
 template <bool T, bool ST>

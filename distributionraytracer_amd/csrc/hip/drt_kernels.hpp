@@ -23,6 +23,8 @@ enum StatSlot : int {
   ST_WAVE_NODE_ITERS, ST_WAVE_PATH_ITERS, ST_LANE_PATH_ITERS,
   // stats builds of the persistent kernel: s_memtime cycles per wave in each loop section
   ST_CYC_REFILL, ST_CYC_NODE, ST_CYC_PROC,
+  // traversal-stack pushes, and those that went past the LDS part of the stack
+  ST_PUSH, ST_PUSH_SPILL,
   ST_COUNT
 };
 
@@ -76,7 +78,7 @@ struct FrameArgs {
   unsigned int* work_counter;  // persistent kernel: next unclaimed work item (zeroed per frame)
   int refill_min;              // persistent kernel: refill a wave once this many lanes are idle
   int process_min;             // persistent kernel: shade once this many lanes have a result
-  int waves;                   // persistent kernel: register budget (waves per SIMD: 2, 3 or 4)
+  int waves;                   // persistent kernel: register budget (waves per SIMD: 5-8)
 };
 
 struct ReduceArgs {
