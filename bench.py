@@ -110,6 +110,7 @@ def main():
     import torch.distributed as dist
 
     import distributionraytracer_amd as drt
+    from distributionraytracer_amd.sharding import FrameGather, TileLayout
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -137,16 +138,19 @@ def main():
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True)
     frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
     if world > 1:
-        _, floats = r.shard_layout(shard_p)
-        shard_buf = torch.empty(floats, dtype=torch.float32, device="cuda")
-        gathered = torch.empty(world * floats, dtype=torch.float32, device="cuda")
+        layout = TileLayout(args.res, args.res, 16, world)
+        tiles, floats = r.shard_layout(shard_p)
+        if floats != layout.floats_per_shard or tiles != len(layout.tiles_of(rank)):
+            raise RuntimeError(f"shard layout mismatch: library {tiles} tiles / {floats} floats, "
+                               f"host {len(layout.tiles_of(rank))} / {layout.floats_per_shard}")
+        fg = FrameGather(layout, device="cuda")
 
     def step(p):
         if world == 1:
             r.render_device(p, frame.data_ptr(), sptr)
         else:
-            r.render_device(p, shard_buf.data_ptr(), sptr)
-            dist.all_gather_into_tensor(gathered, shard_buf)
+            r.render_device(p, fg.shard.data_ptr(), sptr)
+            gathered = fg.gather()  # RCCL all-gather of the shard buffers over xGMI
             if rank == 0:
                 r.unshard_device(shard_p, gathered.data_ptr(), frame.data_ptr(), sptr)
 
@@ -183,6 +187,12 @@ def main():
     dt = float(dt_t.item())
 
     path_ms, total_ms = r.frame_times(args.steps)
+    host_frame_ms = None
+    if world == 1:
+        # PCIe-inclusive variant (not `value`): drt_render with the frame copied to host memory
+        t_h = time.perf_counter()
+        r.render(seed=args.seed)
+        host_frame_ms = (time.perf_counter() - t_h) * 1e3
     kernel_ms = float(np.mean(path_ms)) if len(path_ms) else float("nan")
     bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
@@ -219,6 +229,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "path_kernel<BVH,tri>", "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3)},
+        "host_output_frame_ms": None if host_frame_ms is None else round(host_frame_ms, 3),
         "rays_per_frame": int(rays_frame),
         "samples_per_frame": int(tot["samples"]),
         "msamples_per_s": round(tot["samples"] * args.steps / dt / 1e6, 2),
