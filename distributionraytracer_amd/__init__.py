@@ -206,8 +206,10 @@ class Renderer:
         self.scene = scene
         return self
 
-    def frame_params(self, seed=1, max_depth=4, roughness=0.0, shard=0, n_shards=1, tile=16, stats=False):
+    def frame_params(self, seed=1, max_depth=4, roughness=0.0, shard=0, n_shards=1, tile=16, stats=False,
+                     light_spp=1):
         p = DrtFrameParams()
+        p.light_spp = light_spp
         p.seed = seed
         p.max_depth = max_depth
         p.roughness = roughness
@@ -217,10 +219,10 @@ class Renderer:
         p.flags = FRAME_STATS if stats else 0
         return p
 
-    def render(self, seed=1, max_depth=4, roughness=0.0, stats=False, tile=16):
+    def render(self, seed=1, max_depth=4, roughness=0.0, stats=False, tile=16, light_spp=1):
         info = self.scene.info()
         out = np.zeros((info.res_y, info.res_x, 3), np.float32)
-        p = self.frame_params(seed, max_depth, roughness, tile=tile, stats=stats)
+        p = self.frame_params(seed, max_depth, roughness, tile=tile, stats=stats, light_spp=light_spp)
         check(_lib.load().drt_render(self.h, C.byref(p), _fp(out)), self.h, "drt_render")
         return out
 

@@ -397,6 +397,11 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   F.shard = p->shard;
   F.n_shards = shards;
   F.n_my_tiles = P.n_tiles > p->shard ? (P.n_tiles - p->shard + shards - 1) / shards : 0;
+  if (p->light_spp < 0 || p->light_spp > 4096) DRT_FAIL(c, DRT_E_INVALID, "light_spp %d out of [0, 4096]", p->light_spp);
+  F.light_spp = p->light_spp > 1 ? p->light_spp : 1;
+  F.light_grid = 1;
+  while ((F.light_grid + 1) * (F.light_grid + 1) <= F.light_spp) F.light_grid++;
+  F.light_inv = 1.0f / (float)F.light_spp;
   const bool AA = c->spp != 0;                           // main.cpp:1005-1010
   F.dof = (c->cam.aperture != 0.0f && AA) ? 1 : 0;       // main.cpp:1013-1017
   const bool seq = F.dof || p->roughness != 0.0f;

@@ -302,6 +302,41 @@ __device__ __forceinline__ RayP primary_ray_lens(const SceneArgs& S, V3 lens, fl
   return make_ray(eo, dir);
 }
 
+// ------------------------------------------------------------------------------------------
+// Light loop (main.cpp:383-451) with the light_spp extension: the loop runs over (light, k)
+// pairs j = light * m + k.  A quad light takes m points ((k % g + s.x) / g, (k / g + s.y) / g),
+// g = floor(sqrt(m)), of the pixel's light sample s and each unshadowed Phong term is added
+// scaled by 1/m; a point light takes only k = 0.  With m = 1 this is the reference's loop
+// exactly (point = area_point(s), term scaled by nothing).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ V3 light_point(const drt_light& Lt, V3 ls, int k, const FrameArgs& F) {
+  if (Lt.type != DRT_LIGHT_QUAD) return ld3(Lt.pos);
+  if (F.light_spp > 1) {
+    const int g = F.light_grid;
+    ls = mk(((float)(k % g) + ls.x) / (float)g, ((float)(k / g) + ls.y) / (float)g, 0.0f);
+  }
+  return add(add(ld3(Lt.pos), mul(ld3(Lt.e1), ls.x)), mul(ld3(Lt.e2), ls.y));
+}
+// Phong term of an unshadowed light sample (main.cpp:444-450).
+__device__ __forceinline__ V3 light_term(const drt_material& m, float NdotL, float NdotH, const drt_light& Lt,
+                                         const FrameArgs& F) {
+  const V3 diff = mul(mul(ld3(m.diff), m.kd), NdotL);
+  const V3 spec = mul(mul(ld3(m.spec), m.ks), powf(NdotH, m.shine));
+  V3 c = add(diff, spec);
+  if (F.light_spp > 1 && Lt.type == DRT_LIGHT_QUAD) c = mul(c, F.light_inv);
+  return c;
+}
+// The pair after j (point lights skip k > 0).
+__device__ __forceinline__ int next_light_pair(const SceneArgs& S, const FrameArgs& F, int j) {
+  j++;
+  const int m = F.light_spp;
+  if (m > 1) {
+    const int li = j / m;
+    if (j - li * m > 0 && li < S.n_lights && S.lights[li].type != DRT_LIGHT_QUAD) j = (li + 1) * m;
+  }
+  return j;
+}
+
 // One pending reflection/refraction parent (the C++ call frame of rayTracing, main.cpp:294).
 struct Frame {
   V3 acc, hitP, N, V, lightPos, beer;
@@ -360,21 +395,16 @@ __device__ V3 trace_path(const SceneArgs& S, const FrameArgs& F, RayP q, V3 ls, 
         j = 0;
         after_lights = (S.n_lights == 0);
       }
-    } else {  // result of the shadow query of light j (main.cpp:444-450)
-      if (!hit) {
-        const drt_material& m = S.mats[mat];
-        V3 diff = mul(mul(ld3(m.diff), m.kd), NdotL);
-        V3 spec = mul(mul(ld3(m.spec), m.ks), powf(NdotH, m.shine));
-        acc = add(acc, add(diff, spec));
-      }
-      j++;
-      after_lights = (j >= S.n_lights);
+    } else {  // result of the shadow query of light pair j (main.cpp:444-450)
+      const drt_light& Lt = S.lights[j / F.light_spp];
+      if (!hit) acc = add(acc, light_term(S.mats[mat], NdotL, NdotH, Lt, F));
+      j = next_light_pair(S, F, j);
+      after_lights = (j >= S.n_lights * F.light_spp);
     }
 
-    if (!ret && !after_lights) {  // set up the shadow ray of light j (main.cpp:386-422)
-      const drt_light& L0 = S.lights[j];
-      if (L0.type == DRT_LIGHT_QUAD) lightPos = add(add(ld3(L0.pos), mul(ld3(L0.e1), ls.x)), mul(ld3(L0.e2), ls.y));
-      else lightPos = ld3(L0.pos);
+    if (!ret && !after_lights) {  // set up the shadow ray of light pair j (main.cpp:386-422)
+      const int li = j / F.light_spp;
+      lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
       V3 L = sub(lightPos, hitP);
       V3 Ls = L;
       L = normalize(L);
@@ -818,10 +848,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
 }
 
 template <bool STATS>
-__device__ __forceinline__ void setup_shadow(const SceneArgs& S, Lane& L, Counters& C) {  // main.cpp:386-422
-  const drt_light& Lt = S.lights[L.j];
-  if (Lt.type == DRT_LIGHT_QUAD) L.lightPos = add(add(ld3(Lt.pos), mul(ld3(Lt.e1), L.ls.x)), mul(ld3(Lt.e2), L.ls.y));
-  else L.lightPos = ld3(Lt.pos);
+__device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs& F, Lane& L,
+                                             Counters& C) {  // main.cpp:386-422
+  const int li = L.j / F.light_spp;
+  L.lightPos = light_point(S.lights[li], L.ls, L.j - li * F.light_spp, F);
   V3 Lv = sub(L.lightPos, L.hitP);
   const V3 Ls = Lv;
   Lv = normalize(Lv);
@@ -857,21 +887,16 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       L.lightPos = mk(0, 0, 0);
       L.j = 0;
       if (S.n_lights > 0) {
-        setup_shadow<STATS>(S, L, C);
+        setup_shadow<STATS>(S, F, L, C);
         return;
       }
       after_lights = true;
     }
   } else {  // main.cpp:444-450
-    if (!hit) {
-      const drt_material& m = S.mats[L.mat];
-      const V3 diff = mul(mul(ld3(m.diff), m.kd), L.NdotL);
-      const V3 spec = mul(mul(ld3(m.spec), m.ks), powf(L.NdotH, m.shine));
-      L.acc = add(L.acc, add(diff, spec));
-    }
-    L.j++;
-    if (L.j < S.n_lights) {
-      setup_shadow<STATS>(S, L, C);
+    if (!hit) L.acc = add(L.acc, light_term(S.mats[L.mat], L.NdotL, L.NdotH, S.lights[L.j / F.light_spp], F));
+    L.j = next_light_pair(S, F, L.j);
+    if (L.j < S.n_lights * F.light_spp) {
+      setup_shadow<STATS>(S, F, L, C);
       return;
     }
     after_lights = true;

@@ -71,6 +71,10 @@ struct FrameArgs {
   int nsub;           // work items per pixel
   uint32_t grid_res;  // light 0 gridRes       (main.cpp:684)
   int grid_size;      // (int)sqrt(gridRes)    (main.cpp:689)
+  // light_spp extension: shadow samples per quad light per hit
+  int light_spp;      // m >= 1 (1 = the reference)
+  int light_grid;     // floor(sqrt(m))
+  float light_inv;    // 1.0f / m
   int tile, tiles_x, shard, n_shards, n_my_tiles;
   uint64_t n_items;
   float4* samples;

@@ -131,7 +131,9 @@ typedef struct {
   int32_t n_shards;    /* 1 = whole frame                                               */
   int32_t tile;        /* tile edge in pixels (0 -> 16)                                 */
   int32_t flags;       /* DRT_FRAME_STATS: count rays / node visits / prim tests        */
-  int32_t reserved[5];
+  int32_t light_spp;   /* extension: shadow samples per quad light per
+                          hit, 0 or 1 = the reference (main.cpp:391: one sample)          */
+  int32_t reserved[4];
 } drt_frame_params;
 
 typedef struct {

@@ -732,6 +732,7 @@ struct orc_scene {
   // per-render knobs
   int max_depth = 4;
   float roughness = 0.0f;
+  int light_spp = 1;  // extension: shadow samples per quad light per hit (1 = main.cpp:391)
 
   void add_object(Object o) {
     o.mat = cur_mat;
@@ -870,9 +871,20 @@ C3 orc_scene::ray_tracing(Ray ray, int depth, float ior_1, V3 lightSample, KRng&
   V3 V = neg(ray.d);
   const float offset = 1e-4f;
   V3 lightPos = mk(0, 0, 0);
-  for (int j = 0; j < num_lights; j++) {  // main.cpp:383-451
+  // light_spp extension: a quad light takes m = light_spp points
+  // ((k % g + s.x) / g, (k / g + s.y) / g), g = floor(sqrt(m)), and each unshadowed term is
+  // scaled by 1/m; m = 1 is the reference's loop exactly.
+  int lgrid = 1;
+  while ((lgrid + 1) * (lgrid + 1) <= light_spp) lgrid++;
+  const float linv = 1.0f / (float)light_spp;
+  for (int j = 0; j < num_lights; j++)  // main.cpp:383-451
+  for (int k = 0; k < (lights[j].quad ? light_spp : 1); k++) {
     const Light& light = lights[j];
-    if (light.quad) lightPos = light.area_point(lightSample);
+    V3 ls = lightSample;
+    if (light.quad && light_spp > 1)
+      ls = mk(((float)(k % lgrid) + lightSample.x) / (float)lgrid, ((float)(k / lgrid) + lightSample.y) / (float)lgrid,
+              0.0f);
+    if (light.quad) lightPos = light.area_point(ls);
     else lightPos = light.pos;
     V3 L = sub(lightPos, hitPoint);
     V3 Ls = L;
@@ -895,7 +907,9 @@ C3 orc_scene::ray_tracing(Ray ray, int depth, float ior_1, V3 lightSample, KRng&
     if (!inShadow) {
       C3 diffuseTerm = cmul(cmul(diff_color, kd), NdotL);
       C3 specularTerm = cmul(cmul(spec_color, ks), std::pow(NdotH, shine));  // std::pow(float,float) = powf
-      acc = cadd(acc, cadd(diffuseTerm, specularTerm));
+      C3 term = cadd(diffuseTerm, specularTerm);
+      if (light.quad && light_spp > 1) term = cmul(term, linv);
+      acc = cadd(acc, term);
     }
   }
   if (depth > max_depth) return acc;  // main.cpp:454 (unclamped)
@@ -1347,6 +1361,7 @@ int orc_render(orc_scene* s, uint32_t seed, const orc_options* opt, float* rgb, 
   if (!s->built) orc_scene_build(s);
   s->max_depth = opt ? opt->max_depth : 4;
   s->roughness = opt ? opt->roughness : 0.0f;
+  s->light_spp = (opt && opt->light_spp > 1) ? opt->light_spp : 1;
   const int RX = s->cam.res_x, RY = s->cam.res_y;
   int y0 = 0, y1 = RY;
   if (opt && opt->row_end > opt->row_begin) { y0 = std::max(0, opt->row_begin); y1 = std::min(RY, opt->row_end); }

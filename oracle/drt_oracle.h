@@ -60,6 +60,7 @@ typedef struct {
   float roughness;  /* roughness_param (main.cpp:507) = 0                          */
   int threads;      /* OpenMP threads, 0 = all                                     */
   int row_begin, row_end;  /* render only rows [row_begin,row_end) (bounded sample) */
+  int light_spp;    /* shadow samples per quad light per hit (C3); 0/1 = reference  */
 } orc_options;
 
 /* ---- scene construction ---- */

@@ -47,7 +47,7 @@ class OrcStats(C.Structure):
 
 class OrcOptions(C.Structure):
     _fields_ = [("max_depth", C.c_int), ("roughness", C.c_float), ("threads", C.c_int),
-                ("row_begin", C.c_int), ("row_end", C.c_int)]
+                ("row_begin", C.c_int), ("row_end", C.c_int), ("light_spp", C.c_int)]
 
 
 def build(force: bool = False) -> None:
@@ -317,9 +317,9 @@ class Scene:
         lib().orc_ray_color(self.h, fp(r), fp(ls), len(r), depth, ior, seed, pixel, fp(out))
         return out
 
-    def render(self, seed=1, max_depth=4, roughness=0.0, threads=0, rows=None):
+    def render(self, seed=1, max_depth=4, roughness=0.0, threads=0, rows=None, light_spp=1):
         info = self.info()
-        opt = OrcOptions(max_depth, roughness, threads, rows[0] if rows else 0, rows[1] if rows else 0)
+        opt = OrcOptions(max_depth, roughness, threads, rows[0] if rows else 0, rows[1] if rows else 0, light_spp)
         out = np.zeros((info.res_y, info.res_x, 3), np.float32)
         st = OrcStats()
         rc = lib().orc_render(self.h, seed, C.byref(opt), fp(out), C.byref(st))

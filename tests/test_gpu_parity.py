@@ -113,6 +113,14 @@ RENDER_CASES = {
     "depth8_ext": (lambda: sg.mixed_scene_text(res=(24, 24), spp=4, accel="bvh"), {"max_depth": 8}),
     "tris_soup_bvh": (lambda: sg.synthetic_scene_text(20000, res=(48, 48), spp=4), {}),
     "edge_image_not_multiple_of_tile": (lambda: sg.mixed_scene_text(res=(37, 19), spp=1, accel="bvh"), {}),
+    # light_spp extension: 4 / 3 shadow samples per quad light
+    "soft4_bvh": (lambda: sg.mixed_scene_text(res=(32, 24), spp=4, accel="bvh"), {"light_spp": 4}),
+    "soft3_grid": (lambda: sg.mixed_scene_text(res=(32, 24), spp=4, accel="grid"), {"light_spp": 3}),
+    "soft4_none": (lambda: sg.mixed_scene_text(res=(24, 16), spp=4, accel="none", n_tris=30), {"light_spp": 4}),
+    "soft4_whitted": (lambda: sg.mixed_scene_text(res=(32, 24), spp=0, accel="bvh"), {"light_spp": 4}),
+    "soft4_dof": (lambda: sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", aperture=8.0, focal=1.5),
+                  {"light_spp": 4}),
+    "c3_tris_soft4": (lambda: sg.synthetic_scene_text(20000, res=(40, 40), spp=4), {"light_spp": 4}),
 }
 
 
