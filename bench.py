@@ -160,7 +160,8 @@ def main():
     st = r.stats()
     keys = ["closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_prims", "shadow_prims",
             "closest_leaf", "shadow_leaf", "samples", "wave_node_iters", "wave_path_iters", "lane_path_iters",
-            "cycles_refill", "cycles_node", "cycles_shade", "stack_pushes", "stack_spills"]
+            "cycles_refill", "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
+            "wave_leaf_iters", "cycles_leaf"]
     mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     tot = mine.clone()
     if world > 1:
@@ -240,7 +241,9 @@ def main():
         # fraction of lanes doing useful work in the node loop / in the path loop (wave64)
         "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
                                          tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3),
-                     "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3)},
+                     "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3),
+                     "leaf_block": round((tot["closest_leaf"] + tot["shadow_leaf"]) /
+                                         max(1.0, 64 * tot["wave_leaf_iters"]), 3)},
         # traversal-stack pushes per ray and the share that went past the LDS part (scratch)
         "stack": {"pushes_per_ray": round(tot["stack_pushes"] / max(1.0, rays_frame), 2),
                   "spill_frac": round(tot["stack_spills"] / max(1.0, tot["stack_pushes"]), 4)},
@@ -248,6 +251,9 @@ def main():
         "cycle_share": {k: round(tot["cycles_" + k] / max(1.0, tot["cycles_refill"] + tot["cycles_node"] +
                                                            tot["cycles_shade"]), 3)
                         for k in ("refill", "node", "shade")},
+        # share of the node section spent in the leaf (primitive test) block
+        "leaf_share_of_node": round(tot["cycles_leaf"] / max(1.0, tot["cycles_node"]), 3),
+        "leaf_iter_frac": round(tot["wave_leaf_iters"] / max(1.0, tot["wave_node_iters"]), 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

@@ -50,7 +50,8 @@ class DrtFrameStats(C.Structure):
                                           "shadow_inner", "shadow_leaf", "closest_prims", "shadow_prims",
                                           "samples")] + [("render_ms", C.c_double), ("kernel_ms", C.c_double)] + \
         [(n, C.c_uint64) for n in ("wave_node_iters", "wave_path_iters", "lane_path_iters", "cycles_refill",
-                                   "cycles_node", "cycles_shade", "stack_pushes", "stack_spills")]
+                                   "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
+                                   "wave_leaf_iters", "cycles_leaf")]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_}
@@ -135,10 +136,12 @@ def load():
         # streams and RCCL collectives from torch.distributed interoperate with our kernels.
         import torch  # noqa: F401
 
-        if not LIB_PATH.exists():
-            raise RuntimeError(f"{LIB_PATH} is missing: run distributionraytracer_amd._lib.build() "
+        # DRT_LIBRARY: an alternative build of the same library (A/B runs in tools/ab.sh)
+        path = Path(os.environ.get("DRT_LIBRARY") or LIB_PATH)
+        if not path.exists():
+            raise RuntimeError(f"{path} is missing: run distributionraytracer_amd._lib.build() "
                                "(make -C distributionraytracer_amd/csrc)")
-        L = C.CDLL(str(LIB_PATH))
+        L = C.CDLL(str(path))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res

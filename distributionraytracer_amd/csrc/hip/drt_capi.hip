@@ -567,6 +567,8 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.cycles_shade = s[ST_CYC_PROC];
       c->last.stack_pushes = s[ST_PUSH];
       c->last.stack_spills = s[ST_PUSH_SPILL];
+      c->last.wave_leaf_iters = s[ST_WAVE_LEAF_ITERS];
+      c->last.cycles_leaf = s[ST_CYC_LEAF];
     }
   }
   *out = c->last;

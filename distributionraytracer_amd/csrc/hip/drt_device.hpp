@@ -215,6 +215,19 @@ __device__ __forceinline__ bool hit_box(const float4& q0, const float4& q1, cons
   return false;
 }
 
+// Object::hit on an already loaded record (q2 is only read for triangles).
+template <bool TRI_ONLY>
+__device__ __forceinline__ bool hit_prim_rec(const float4& q0, const float4& q1, const float4& q2, const RayP& r,
+                                             float& t) {
+  if (TRI_ONLY) return hit_triangle(q0, q1, q2, r, t);
+  switch (prim_type(q0)) {
+    case PRIM_TRIANGLE: return hit_triangle(q0, q1, q2, r, t);
+    case PRIM_SPHERE: return hit_sphere(q0, q1, r, t);
+    case PRIM_PLANE: return hit_plane(q0, q1, r, t);
+    default: return hit_box(q0, q1, r, t);
+  }
+}
+
 template <bool TRI_ONLY>
 __device__ __forceinline__ bool hit_prim(const float4* __restrict__ prims, uint32_t i, const RayP& r, float& t) {
   const float4 q0 = prims[3 * i];

@@ -326,6 +326,10 @@ __device__ __forceinline__ V3 light_term(const drt_material& m, float NdotL, flo
   if (F.light_spp > 1 && Lt.type == DRT_LIGHT_QUAD) c = mul(c, F.light_inv);
   return c;
 }
+// Light index of pair j (no integer division in the reference case m = 1).
+__device__ __forceinline__ int light_of_pair(int j, const FrameArgs& F) {
+  return F.light_spp == 1 ? j : j / F.light_spp;
+}
 // The pair after j (point lights skip k > 0).
 __device__ __forceinline__ int next_light_pair(const SceneArgs& S, const FrameArgs& F, int j) {
   j++;
@@ -396,14 +400,14 @@ __device__ V3 trace_path(const SceneArgs& S, const FrameArgs& F, RayP q, V3 ls, 
         after_lights = (S.n_lights == 0);
       }
     } else {  // result of the shadow query of light pair j (main.cpp:444-450)
-      const drt_light& Lt = S.lights[j / F.light_spp];
+      const drt_light& Lt = S.lights[light_of_pair(j, F)];
       if (!hit) acc = add(acc, light_term(S.mats[mat], NdotL, NdotH, Lt, F));
       j = next_light_pair(S, F, j);
       after_lights = (j >= S.n_lights * F.light_spp);
     }
 
     if (!ret && !after_lights) {  // set up the shadow ray of light pair j (main.cpp:386-422)
-      const int li = j / F.light_spp;
+      const int li = light_of_pair(j, F);
       lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
       V3 L = sub(lightPos, hitP);
       V3 Ls = L;
@@ -698,6 +702,9 @@ struct Lane {
   uint32_t hitPrim, mat;
   int j;
 };
+// (Measured alternative, kept out: the shading state in a private per-activation frame array
+// instead of registers — the extra scratch stores sit in vmcnt ahead of the next node fetch,
+// 9 % slower.)
 
 // AABB::hit + isInside (boundingBox.cpp:41-44, :64-124; bvh.cpp:256-257) for a ray whose origin
 // and slab constants are finite.  Every slab product is then finite and, because a child box has
@@ -742,88 +749,108 @@ __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const R
   L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (ray_finite(q) ? LF_FINITE : 0u);
 }
 
+__device__ __forceinline__ uint64_t stamp_cycles() {
+  __builtin_amdgcn_sched_barrier(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 // One iteration of the node loop of bvh.cpp:245-312 / :331-388: visit node `cur` (both child
 // boxes of an inner node, or every primitive of a leaf), then — if the visit produced no next
 // node — make ONE pop attempt.  A closest-hit pop that is pruned (t >= best, bvh.cpp:303) leaves
 // LF_POP set, so the next iteration tries the next entry; the visit order is exactly the
 // reference's, only spread over iterations with uniform, short control flow.
+// (Measured alternative, kept out: one primitive per iteration with a fetch shared by node and
+// leaf lanes — fewer leaf-block cycles but more iterations, 3 % slower overall.)
 template <bool TRI_ONLY, bool STATS, int CAP>
 __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* lds, uint32_t* ov_desc,
-                                          float* ov_t, bool wave_finite, Counters& C) {
+                                          float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kBlock * 4u;  // desc part; the t part follows
   uint32_t fl = L.fl;
   const bool shadow = (fl & LF_SHADOW) != 0u;
-  if (!(fl & LF_POP)) {
-    const uint32_t cur = L.cur;
-    if (!desc_is_leaf(cur)) {
-      if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
-      const float4* nd = S.nodes + 4 * (size_t)cur;
-      const float4 a = nd[0], b = nd[1], c = nd[2];
-      const uint4 d = *reinterpret_cast<const uint4*>(nd + 3);
-      float tL, tR;
-      bool hL, hR;
-      if (wave_finite) {
-        hL = box_test_finite(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
-        hR = box_test_finite(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
-      } else {
-        hL = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
-        hR = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
-        if (box_inside(a.x, a.y, a.z, a.w, b.x, b.y, L.q.o)) tL = 0.0f;
-        if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, L.q.o)) tR = 0.0f;
-      }
-      const bool both = hL && hR;
-      // shadow: tL <= tR, closest: tL < tR (bvh.cpp:262 / :344).  Only consulted when both boxes
-      // are hit, and then tL, tR are non-NaN and >= 0 (or -0), so they order as sign-cleared
-      // integers and `<=` is `< + 1`.
-      const uint32_t uL = __float_as_uint(tL) & 0x7fffffffu, uR = __float_as_uint(tR) & 0x7fffffffu;
-      const bool left_first = uL < uR + (fl & LF_SHADOW);
-      L.cur = (hL && (left_first || !hR)) ? d.x : d.y;
-      fl |= (hL | hR) ? 0u : LF_POP;
-      // push the far child (bvh.cpp:268-283); the LDS slot above the top is free, so the store
-      // is unconditional and only the stack pointer depends on `both`
-      const uint32_t pd = left_first ? d.y : d.x;
-      const float pt = left_first ? tR : tL;
-      const uint32_t spa = L.spa;
-      if (spa < kLdsBytes) {
-        *(LdsU32*)(lds + spa) = pd;
-        *(LdsF32*)(lds + kLdsBytes + spa) = pt;
-      } else if (both) {
-        ov_desc[(spa >> 10) - CAP] = pd;
-        ov_t[(spa >> 10) - CAP] = pt;
-      }
-      L.spa = spa + (both ? 1024u : 0u);
-      if (STATS && both) {
-        C.v[ST_PUSH]++;
-        if (spa >= kLdsBytes) C.v[ST_PUSH_SPILL]++;
-      }
+  const uint32_t cur = L.cur;
+  const bool visit = !(fl & LF_POP);
+  // the inner-node and leaf visits are two consecutive exec-masked blocks (as compiled anyway);
+  // stats builds time the leaf block
+  if (visit && !desc_is_leaf(cur)) {
+    if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
+    const float4* nd = S.nodes + 4 * (size_t)cur;
+    const float4 a = nd[0], b = nd[1], c = nd[2];
+    const uint4 d = *reinterpret_cast<const uint4*>(nd + 3);
+    float tL, tR;
+    bool hL, hR;
+    if (wave_finite) {
+      hL = box_test_finite(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
+      hR = box_test_finite(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
     } else {
-      if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
-      uint32_t first = desc_first(cur), cnt = desc_count(cur);
-      if (cnt == kBigLeaf) {
-        const uint2 bl = S.big_leaves[first];
-        first = bl.x;
-        cnt = bl.y;
-      }
-      for (uint32_t i = 0; i < cnt; i++) {
-        if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
-        float t;
-        if (hit_prim<TRI_ONLY>(S.prims, first + i, L.q, t)) {
-          if (shadow) {
-            if (t <= L.thr) {  // any-hit: done (bvh.cpp:376-377)
-              L.fl = (fl | LF_HIT) & ~LF_TRAV;
-              return;
-            }
-          } else if (t < L.best_t) {
-            L.best_t = t;
-            L.best_prim = first + i;
-            fl |= LF_HIT;
-          }
-        }
-      }
-      fl |= LF_POP;
+      hL = box_hit(a.x, a.y, a.z, a.w, b.x, b.y, L.q, tL);
+      hR = box_hit(b.z, b.w, c.x, c.y, c.z, c.w, L.q, tR);
+      if (box_inside(a.x, a.y, a.z, a.w, b.x, b.y, L.q.o)) tL = 0.0f;
+      if (box_inside(b.z, b.w, c.x, c.y, c.z, c.w, L.q.o)) tR = 0.0f;
+    }
+    const bool both = hL && hR;
+    // shadow: tL <= tR, closest: tL < tR (bvh.cpp:262 / :344).  Only consulted when both boxes
+    // are hit, and then tL, tR are non-NaN and >= 0 (or -0), so they order as sign-cleared
+    // integers and `<=` is `< + 1`.
+    const uint32_t uL = __float_as_uint(tL) & 0x7fffffffu, uR = __float_as_uint(tR) & 0x7fffffffu;
+    const bool left_first = uL < uR + (fl & LF_SHADOW);
+    L.cur = (hL && (left_first || !hR)) ? d.x : d.y;
+    fl |= (hL | hR) ? 0u : LF_POP;
+    // push the far child (bvh.cpp:268-283); the LDS slot above the top is free, so the store
+    // is unconditional and only the stack pointer depends on `both`
+    const uint32_t pd = left_first ? d.y : d.x;
+    const float pt = left_first ? tR : tL;
+    const uint32_t spa = L.spa;
+    if (spa < kLdsBytes) {
+      *(LdsU32*)(lds + spa) = pd;
+      *(LdsF32*)(lds + kLdsBytes + spa) = pt;
+    } else if (both) {
+      ov_desc[(spa >> 10) - CAP] = pd;
+      ov_t[(spa >> 10) - CAP] = pt;
+    }
+    L.spa = spa + (both ? 1024u : 0u);
+    if (STATS && both) {
+      C.v[ST_PUSH]++;
+      if (spa >= kLdsBytes) C.v[ST_PUSH_SPILL]++;
     }
   }
-  if (fl & LF_POP) {  // bvh.cpp:299-311 / :381-387
+  const bool leaf = visit && desc_is_leaf(cur);
+  uint64_t t0 = 0;
+  if (STATS) {
+    t0 = stamp_cycles();
+    if (__ballot(leaf) != 0 && (threadIdx.x & 63u) == 0) C.v[ST_WAVE_LEAF_ITERS]++;
+  }
+  if (leaf) {
+    if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
+    uint32_t first = desc_first(cur), cnt = desc_count(cur);
+    if (cnt == kBigLeaf) {
+      const uint2 bl = S.big_leaves[first];
+      first = bl.x;
+      cnt = bl.y;
+    }
+    // (Measured alternative, kept out: fetching primitive records in pairs before testing —
+    // cheaper leaves, but the extra live registers force spills at 6 waves/SIMD.)
+    for (uint32_t i = 0; i < cnt; i++) {
+      if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+      float t;
+      if (hit_prim<TRI_ONLY>(S.prims, first + i, L.q, t)) {
+        if (shadow) {
+          if (t <= L.thr) {  // any-hit: done (bvh.cpp:376-377)
+            fl = (fl | LF_HIT) & ~LF_TRAV;
+            break;
+          }
+        } else if (t < L.best_t) {
+          L.best_t = t;
+          L.best_prim = first + i;
+          fl |= LF_HIT;
+        }
+      }
+    }
+    if (fl & LF_TRAV) fl |= LF_POP;
+  }
+  if (STATS) cyc_leaf += stamp_cycles() - t0;
+  if ((fl & (LF_POP | LF_TRAV)) == (LF_POP | LF_TRAV)) {  // bvh.cpp:299-311 / :381-387
     if (L.spa < 1024u) {
       fl &= ~LF_TRAV;
     } else {
@@ -850,7 +877,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
 template <bool STATS>
 __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs& F, Lane& L,
                                              Counters& C) {  // main.cpp:386-422
-  const int li = L.j / F.light_spp;
+  const int li = light_of_pair(L.j, F);
   L.lightPos = light_point(S.lights[li], L.ls, L.j - li * F.light_spp, F);
   V3 Lv = sub(L.lightPos, L.hitP);
   const V3 Ls = Lv;
@@ -893,7 +920,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       after_lights = true;
     }
   } else {  // main.cpp:444-450
-    if (!hit) L.acc = add(L.acc, light_term(S.mats[L.mat], L.NdotL, L.NdotH, S.lights[L.j / F.light_spp], F));
+    if (!hit) L.acc = add(L.acc, light_term(S.mats[L.mat], L.NdotL, L.NdotH, S.lights[light_of_pair(L.j, F)], F));
     L.j = next_light_pair(S, F, L.j);
     if (L.j < S.n_lights * F.light_spp) {
       setup_shadow<STATS>(S, F, L, C);
@@ -1040,7 +1067,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t n_items = (uint32_t)F.n_items;
   bool exhausted = false;  // wave-uniform
-  uint64_t cyc[3] = {0, 0, 0};  // stats builds: refill / node / shading section cycles (wave-uniform)
+  uint64_t cyc[4] = {0, 0, 0, 0};  // stats builds: refill / node / shading / leaf-block cycles (wave-uniform)
   auto stamp = [&]() -> uint64_t {
     if (!STATS) return 0;
     __builtin_amdgcn_sched_barrier(0);
@@ -1077,7 +1104,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
     if (trav) {
       if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
       const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
-      if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C);
+      if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
     }
     const uint64_t t2 = stamp();
     // ---- batched shading for lanes whose query completed
@@ -1101,6 +1128,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
     atomicAdd(&F.stats[ST_CYC_REFILL], (unsigned long long)cyc[0]);
     atomicAdd(&F.stats[ST_CYC_NODE], (unsigned long long)cyc[1]);
     atomicAdd(&F.stats[ST_CYC_PROC], (unsigned long long)cyc[2]);
+    atomicAdd(&F.stats[ST_CYC_LEAF], (unsigned long long)cyc[3]);
   }
 }
 

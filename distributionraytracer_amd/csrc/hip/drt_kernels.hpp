@@ -25,6 +25,8 @@ enum StatSlot : int {
   ST_CYC_REFILL, ST_CYC_NODE, ST_CYC_PROC,
   // traversal-stack pushes, and those that went past the LDS part of the stack
   ST_PUSH, ST_PUSH_SPILL,
+  // node loop: wave iterations that ran the leaf block, and s_memtime cycles spent in it
+  ST_WAVE_LEAF_ITERS, ST_CYC_LEAF,
   ST_COUNT
 };
 

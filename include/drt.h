@@ -148,6 +148,7 @@ typedef struct {
   uint64_t wave_path_iters, lane_path_iters; /* path-loop iterations per wave / per lane  */
   uint64_t cycles_refill, cycles_node, cycles_shade; /* persistent kernel: s_memtime cycles */
   uint64_t stack_pushes, stack_spills;   /* traversal-stack pushes / those beyond the LDS part */
+  uint64_t wave_leaf_iters, cycles_leaf; /* node-loop iterations that ran the leaf block / its cycles */
 } drt_frame_stats;
 
 int drt_create(drt_ctx** out, const drt_options* opt);
