@@ -829,12 +829,21 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
       first = bl.x;
       cnt = bl.y;
     }
-    // (Measured alternative, kept out: fetching primitive records in pairs before testing —
-    // cheaper leaves, but the extra live registers force spills at 6 waves/SIMD.)
-    for (uint32_t i = 0; i < cnt; i++) {
+    // primitives in pairs: both records are fetched before the first test, so a two-primitive
+    // leaf costs one memory round trip; tests (and the shadow early exit) stay in order
+    const float4* pr = S.prims + 3 * (size_t)first;
+    for (uint32_t i = 0; i < cnt; i += 2) {
+      const bool two = i + 1 < cnt;
+      const float4 p0 = pr[3 * i], p1 = pr[3 * i + 1], p2 = pr[3 * i + 2];
+      float4 r0, r1, r2;
+      if (two) {
+        r0 = pr[3 * i + 3];
+        r1 = pr[3 * i + 4];
+        r2 = pr[3 * i + 5];
+      }
       if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
       float t;
-      if (hit_prim<TRI_ONLY>(S.prims, first + i, L.q, t)) {
+      if (hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t)) {
         if (shadow) {
           if (t <= L.thr) {  // any-hit: done (bvh.cpp:376-377)
             fl = (fl | LF_HIT) & ~LF_TRAV;
@@ -843,6 +852,20 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
         } else if (t < L.best_t) {
           L.best_t = t;
           L.best_prim = first + i;
+          fl |= LF_HIT;
+        }
+      }
+      if (!two) break;
+      if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+      if (hit_prim_rec<TRI_ONLY>(r0, r1, r2, L.q, t)) {
+        if (shadow) {
+          if (t <= L.thr) {
+            fl = (fl | LF_HIT) & ~LF_TRAV;
+            break;
+          }
+        } else if (t < L.best_t) {
+          L.best_t = t;
+          L.best_prim = first + i + 1;
           fl |= LF_HIT;
         }
       }
