@@ -46,9 +46,10 @@ def synthetic_triangles(n, seed=1):
     return np.concatenate([v.astype(np.float32).reshape(n, 9), FLOOR])
 
 
-def populate(scene, tris, res, spp):
+def populate(scene, tris, res, spp, aperture=0.0, focal=1.0):
     """Same calls for the product scene and the oracle scene (P3F-equivalent content)."""
-    scene.set_camera(CAMERA["eye"], CAMERA["at"], CAMERA["up"], CAMERA["fovy"], CAMERA["hither"], res, res, 0.0, 1.0)
+    scene.set_camera(CAMERA["eye"], CAMERA["at"], CAMERA["up"], CAMERA["fovy"], CAMERA["hither"], res, res,
+                     aperture, focal)
     scene.set_background((0.078, 0.361, 0.753))
     scene.set_accel("bvh")
     scene.set_spp(spp)
@@ -58,25 +59,26 @@ def populate(scene, tris, res, spp):
     scene.add_triangles(tris)
 
 
-def cpu_baseline(tris, res, spp, seed, target_s, threads):
+def cpu_baseline(tris, res, spp, seed, target_s, threads, ext):
     """The CPU oracle (C++/OpenMP restatement of the reference, oracle/) timed on this host on a
     bounded sample: a band of full rows of the SAME frame."""
     from oracle import oracle as O
 
     O.build()
     s = O.Scene.new()
-    populate(s, tris, res, spp)
+    populate(s, tris, res, spp, ext["aperture"], ext["focal"])
+    kw = {k: ext[k] for k in ("max_depth", "roughness", "light_spp")}
     t0 = time.time()
     s.build()
     build_s = time.time() - t0
     mid = res // 2
     t0 = time.time()
-    _, st = s.render(seed=seed, threads=threads, rows=(mid, mid + 1))
+    _, st = s.render(seed=seed, threads=threads, rows=(mid, mid + 1), **kw)
     per_row = max(time.time() - t0, 1e-3)
     rows = int(max(1, min(res, target_s / per_row)))
     y0 = max(0, mid - rows // 2)
     t0 = time.time()
-    _, st = s.render(seed=seed, threads=threads, rows=(y0, y0 + rows))
+    _, st = s.render(seed=seed, threads=threads, rows=(y0, y0 + rows), **kw)
     dt = time.time() - t0
     rays = st["closest_calls"] + st["shadow_calls"]
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
@@ -94,6 +96,12 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--seed", type=int, default=1)
+    # BASELINE configs C3/C4; defaults are the headline workload
+    ap.add_argument("--aperture", type=float, default=0.0, help="thin-lens aperture ratio (C4: 8)")
+    ap.add_argument("--focal", type=float, default=1.0, help="focal ratio (C4: 1)")
+    ap.add_argument("--roughness", type=float, default=0.0, help="glossy reflection (C4: 0.1)")
+    ap.add_argument("--max-depth", type=int, default=4, help="MAX_DEPTH (C4: 8)")
+    ap.add_argument("--light-spp", type=int, default=1, help="shadow samples per quad light (C3: 4)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
@@ -123,7 +131,9 @@ def main():
     t0 = time.time()
     tris = synthetic_triangles(args.tris, args.seed)
     scene = drt.Scene()
-    populate(scene, tris, args.res, args.spp)
+    ext = {"aperture": args.aperture, "focal": args.focal, "roughness": args.roughness,
+           "max_depth": args.max_depth, "light_spp": args.light_spp}
+    populate(scene, tris, args.res, args.spp, args.aperture, args.focal)
     scene.build()
     info = scene.info()
     build_s = time.time() - t0
@@ -134,8 +144,9 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
-    shard_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world)
-    stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True)
+    fkw = {"max_depth": args.max_depth, "roughness": args.roughness, "light_spp": args.light_spp}
+    shard_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, **fkw)
+    stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
     frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
     if world > 1:
         layout = TileLayout(args.res, args.res, 16, world)
@@ -192,18 +203,21 @@ def main():
     if world == 1:
         # PCIe-inclusive variant (not `value`): drt_render with the frame copied to host memory
         t_h = time.perf_counter()
-        r.render(seed=args.seed)
+        r.render(seed=args.seed, **fkw)
         host_frame_ms = (time.perf_counter() - t_h) * 1e3
     kernel_ms = float(np.mean(path_ms)) if len(path_ms) else float("nan")
     bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
+    extras = [f"{k}{v:g}" for k, v in ext.items()
+              if v != {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1}[k]]
+    workload_key = "_".join([f"tris{args.tris}_res{args.res}_spp{args.spp}"] + extras)
     tj = Path(args.traffic_json)
     if world == 1 and tj.exists():
         try:
             tr = json.loads(tj.read_text())
-            if tr.get("workload") == f"tris{args.tris}_res{args.res}_spp{args.spp}":
+            if tr.get("workload") == workload_key:
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -223,8 +237,11 @@ def main():
         "dtype": "f32",
         "data": "synthetic (seeded random triangle soup, SURVEY.md §8d)",
         "config": {"workload": f"synthetic {args.tris} triangles + floor, BVH, {args.res}x{args.res}, "
-                               f"{args.spp} spp, MAX_DEPTH 4, 1 quad + 1 point light",
-                   "tris": args.tris, "res": args.res, "spp": args.spp, "accel": "bvh",
+                               f"{args.spp} spp, MAX_DEPTH {args.max_depth}, 1 quad + 1 point light"
+                               + (f", DoF aperture {args.aperture:g} focal {args.focal:g}" if args.aperture else "")
+                               + (f", roughness {args.roughness:g}" if args.roughness else "")
+                               + (f", {args.light_spp} quad-light samples" if args.light_spp > 1 else ""),
+                   "tris": args.tris, "res": args.res, "spp": args.spp, "accel": "bvh", "key": workload_key,
                    "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -258,7 +275,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(tris, args.res, args.spp, args.seed, args.cpu_seconds, threads)
+            out["cpu_baseline"] = cpu_baseline(tris, args.res, args.spp, args.seed, args.cpu_seconds, threads, ext)
             out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         except Exception as e:  # the baseline is reported, never required
             out["cpu_baseline"] = {"value": None, "error": repr(e)}

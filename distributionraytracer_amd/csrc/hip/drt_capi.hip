@@ -375,6 +375,8 @@ struct Plan {
   FrameArgs F;
   ReduceArgs R;
   int tiles_y, n_tiles;
+  bool persistent;      // path_persistent (BVH) instead of path_kernel
+  uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
 
 static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
@@ -422,10 +424,17 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
     F.mode = seq ? MODE_SEQ : MODE_WHITTED_POINT;
     F.nsub = 1;
   }
-  const int per_pixel = F.mode == MODE_SEQ ? 1 : F.nsub;
+  P.persistent = persistent_supported(c->accel, F.mode) && env_int("DRT_PERSISTENT", 1) != 0;
+  const int per_pixel = F.mode == MODE_SEQ ? 1 : F.nsub;  // work items per pixel
+  int slots = per_pixel;                                   // sample slots per pixel
+  if (P.persistent && F.mode == MODE_SEQ) {  // a lane runs a pixel's samples in order, one slot each
+    slots = c->spp ? (int)c->spp : (F.grid_res ? (int)F.grid_res : 1);
+    F.nsub = slots;
+  }
   F.n_items = (uint64_t)F.n_my_tiles * F.tile * F.tile * per_pixel;
+  P.n_slots = (uint64_t)F.n_my_tiles * F.tile * F.tile * slots;
   ReduceArgs& R = P.R;
-  R.nsub = per_pixel;
+  R.nsub = slots;
   R.scale = scale;
   R.tile = F.tile; R.tiles_x = F.tiles_x; R.shard = F.shard; R.n_shards = F.n_shards; R.n_my_tiles = F.n_my_tiles;
   R.res_x = RX; R.res_y = RY;
@@ -440,7 +449,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   rc = scene_args(c, c->accel, S);
   if (rc) return rc;
   DRT_HIP(c, hipSetDevice(c->device));
-  DRT_HIP(c, c->d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.F.n_items)));
+  DRT_HIP(c, c->d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.n_slots)));
   DRT_HIP(c, c->d_stats.ensure(sizeof(unsigned long long) * ST_COUNT));
   const bool stats = (p->flags & DRT_FRAME_STATS) != 0;
   c->stats_valid = stats;
@@ -453,7 +462,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
   c->frames++;
   DRT_HIP(c, hipEventRecord(ev[0], st));
-  const bool persistent = persistent_supported(c->accel, P.F.mode) && env_int("DRT_PERSISTENT", 1) != 0;
+  const bool persistent = P.persistent;
   if (persistent) {
     DRT_HIP(c, c->d_counter.ensure(256));
     DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 256, st));

@@ -650,7 +650,8 @@ __global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) 
 }
 
 // ------------------------------------------------------------------------------------------
-// Persistent BVH path kernel (modes without RNG in the path: AA, Whitted quad/point).
+// Persistent BVH path kernel (all frame modes; MODE_SEQ runs a pixel's samples in order on one
+// lane because its keyed stream is consumed in call order).
 //
 // Each lane runs rayTracing()'s DFS as an explicit state machine and every loop iteration
 // does ONE unit of work per lane: a BVH node step (inner node, or leaf + stack pops) for lanes
@@ -701,6 +702,9 @@ struct Lane {
   float NdotL, NdotH, hitT;
   uint32_t hitPrim, mat;
   int j;
+  // MODE_SEQ only (dead otherwise): the lane owns a pixel and runs its samples in order on the
+  // pixel's keyed stream — sample index, next rand() call index, pixel key
+  uint32_t smp, rk, pmix;
 };
 // (Measured alternative, kept out: the shading state in a private per-activation frame array
 // instead of registers — the extra scratch stores sit in vmcnt ahead of the next node fetch,
@@ -913,8 +917,25 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
                      C);
 }
 
-// Consume the completed query of lane L (main.cpp:294-521 between two traversals).
+// reflectDir (main.cpp:504-508); MODE_SEQ draws rnd_unit_sphere on the lane's keyed stream
+// exactly where the reference calls it, whatever the roughness (Q15)
+template <int MODE>
+__device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 V) {
+  V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
+  if (MODE == MODE_SEQ) {
+    KRng rng{F.seed, L.pmix, L.rk};
+    R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
+    L.rk = rng.k;
+    return R;
+  }
+  return normalize(R);
+}
+
 template <bool STATS>
+__device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C);
+
+// Consume the completed query of lane L (main.cpp:294-521 between two traversals).
+template <bool STATS, int MODE>
 __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Frame* fr, Counters& C) {
   const float offset = 1e-4f;
   V3 c = mk(0, 0, 0);
@@ -994,7 +1015,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         f.ior1 = L.ior1; f.kr = kr; f.mat = L.mat;
         f.flags = (has_refr ? 0u : 1u) | (outside ? 2u : 0u) | (has_refl ? 4u : 0u);
         if (!has_refr) {
-          const V3 R = normalize(sub(mul(mul(L.N, dot(L.V, L.N)), 2.0f), L.V));
+          const V3 R = reflect_dir<MODE>(F, L, L.N, L.V);
           if (dot(R, L.N) > 0.0f) f.flags |= 8u;
           child = make_ray(add(L.hitP, mul(L.N, offset)), R);
           child_ior = L.ior1;
@@ -1017,7 +1038,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       f.acc = add(f.acc, mul(rc, 1.0f - f.kr));
       if (f.flags & 4u) {
         f.flags |= 1u;
-        const V3 R = normalize(sub(mul(mul(f.N, dot(f.V, f.N)), 2.0f), f.V));
+        const V3 R = reflect_dir<MODE>(F, L, f.N, f.V);
         if (dot(R, f.N) > 0.0f) f.flags |= 8u;
         L.ior1 = f.ior1;
         L.ls = f.lightPos;
@@ -1034,14 +1055,70 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       L.fsp--;
     }
   }
+  if (MODE == MODE_SEQ) {  // sample smp of the lane's pixel is done: next sample, same stream
+    F.samples[(size_t)L.item * F.nsub + L.smp] = make_float4(c.x, c.y, c.z, 0.0f);
+    if (++L.smp < (uint32_t)F.nsub) {
+      seq_start_sample<STATS>(S, F, L, C);
+      return;
+    }
+    L.item = kNoItem;
+    return;
+  }
   F.samples[L.item] = make_float4(c.x, c.y, c.z, 0.0f);  // rayTracing(depth = 1) returned
   L.item = kNoItem;
+}
+
+// MODE_SEQ: start sample L.smp of pixel L.item (path_kernel's in-order loop, main.cpp:651-665,
+// or the Whitted light-sample loop with glossy reflection, main.cpp:683-697).  The samples of
+// a pixel go to samples[pixel * nsub + smp]; the ordered reduce sums them as the loop did.
+template <bool STATS>
+__device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
+  const Item it = decode_item(F, S.res_x, S.res_y, L.item, 1);
+  L.depth = 1;
+  L.fsp = 0;
+  L.ior1 = 1.0f;
+  L.fl = 0u;
+  if (STATS) C.v[ST_SAMPLES]++;
+  RayP r;
+  if (F.spp > 0) {
+    float rx, ry, sx, sy;
+    sample_prologue(F, L.pmix, (int)L.smp, rx, ry, sx, sy);
+    const float px = (float)it.x + rx, py = (float)it.y + ry;
+    if (F.dof) {
+      KRng rng{F.seed, L.pmix, L.rk};
+      r = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
+      L.rk = rng.k;
+    } else {
+      r = primary_ray(S, px, py);
+    }
+    L.ls = mk(sx, sy, 0.0f);
+  } else {
+    const int s = (int)L.smp;
+    r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
+    L.ls = F.grid_res ? mk(((float)(s % F.grid_size) + 0.5f) / (float)F.grid_size,
+                           ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
+                      : mk(0.5f, 0.5f, 0.0f);
+  }
+  start_query<STATS>(S, L, r, false, 0.0f, C);
 }
 
 template <bool STATS, int MODE>
 __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item,
                                           Counters& C) {
   L.item = item;
+  if (MODE == MODE_SEQ) {  // work item = pixel
+    const Item it = decode_item(F, S.res_x, S.res_y, item, 1);
+    if (!it.valid) {  // padding of a partial tile
+      for (int k = 0; k < F.nsub; k++) F.samples[(size_t)item * F.nsub + k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      L.item = kNoItem;
+      return;
+    }
+    L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+    L.smp = 0;
+    L.rk = F.spp > 0 ? 5u * F.spp - 1u : 0u;  // after the prologue's 4 spp + spp - 1 calls
+    seq_start_sample<STATS>(S, F, L, C);
+    return;
+  }
   const int per_pixel = F.nsub;
   const Item it = decode_item(F, S.res_x, S.res_y, item, per_pixel);
   if (!it.valid) {  // padding of a partial tile
@@ -1137,7 +1214,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
         if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
         if (done) C.v[ST_LANE_PATH_ITERS]++;
       }
-      if (done) lane_process<STATS>(S, F, L, fr, C);
+      if (done) lane_process<STATS, MODE>(S, F, L, fr, C);
     }
     if (STATS) {
       const uint64_t t3 = stamp();
@@ -1285,11 +1362,12 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
   switch (F.mode) {
     case MODE_AA: launch_persistent_m<T, ST, MODE_AA>(S, F, st); break;
     case MODE_WHITTED_QUAD: launch_persistent_m<T, ST, MODE_WHITTED_QUAD>(S, F, st); break;
+    case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT>(S, F, st); break;
   }
 }
 
-bool persistent_supported(int accel, int mode) { return accel == ACC_BVH && mode != MODE_SEQ; }
+bool persistent_supported(int accel, int mode) { return accel == ACC_BVH; }
 
 void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, bool tri_only, bool stats, hipStream_t st) {
   if (tri_only) { if (stats) launch_persistent_t<true, true>(S, F, st); else launch_persistent_t<true, false>(S, F, st); }

@@ -121,6 +121,12 @@ RENDER_CASES = {
     "soft4_dof": (lambda: sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", aperture=8.0, focal=1.5),
                   {"light_spp": 4}),
     "c3_tris_soft4": (lambda: sg.synthetic_scene_text(20000, res=(40, 40), spp=4), {"light_spp": 4}),
+    # in-order (keyed-stream) modes on the persistent BVH kernel: Whitted with glossy reflection
+    "whitted_glossy_quad_bvh": (lambda: sg.mixed_scene_text(res=(24, 16), spp=0, accel="bvh"), {"roughness": 0.2}),
+    "whitted_glossy_point_bvh": (lambda: sg.mixed_scene_text(res=(24, 16), spp=0, accel="bvh", quad=False),
+                                 {"roughness": 0.2}),
+    "dof_glossy_depth8_bvh": (lambda: sg.mixed_scene_text(res=(24, 16), spp=9, accel="bvh", aperture=8.0,
+                                                          focal=1.5), {"roughness": 0.1, "max_depth": 8}),
 }
 
 
