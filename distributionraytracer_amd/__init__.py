@@ -37,6 +37,21 @@ def _fp(a):
     return a.ctypes.data_as(_lib._f)
 
 
+def image_rgb8(frame):
+    """u8fromfloat of a (RES_Y, RES_X, 3) float frame, row 0 = bottom (main.cpp:716-718)."""
+    f = np.ascontiguousarray(frame, np.float32)
+    out = np.empty(f.shape, np.uint8)
+    check(_lib.load().drt_image_rgb8(f.ctypes.data, f.shape[1], f.shape[0], out.ctypes.data), what="drt_image_rgb8")
+    return out
+
+
+def write_png(path, frame):
+    """saveImgFile (main.cpp:251-266): 8-bit RGB PNG, displayed upright (top row = frame row RES_Y-1)."""
+    f = np.ascontiguousarray(frame, np.float32)
+    check(_lib.load().drt_image_write_png(str(path).encode(), f.ctypes.data, f.shape[1], f.shape[0]),
+          what="drt_image_write_png")
+
+
 def load_skybox_dir(path, max_size=None):
     """Decode the six cube faces (DevIL in the reference, scene.cpp:329-378) with PIL, rows
     bottom-up (IL_ORIGIN_LOWER_LEFT)."""
@@ -207,9 +222,10 @@ class Renderer:
         return self
 
     def frame_params(self, seed=1, max_depth=4, roughness=0.0, shard=0, n_shards=1, tile=16, stats=False,
-                     light_spp=1):
+                     light_spp=1, progressive_frame=0):
         p = DrtFrameParams()
         p.light_spp = light_spp
+        p.progressive_frame = progressive_frame
         p.seed = seed
         p.max_depth = max_depth
         p.roughness = roughness
@@ -219,10 +235,19 @@ class Renderer:
         p.flags = FRAME_STATS if stats else 0
         return p
 
-    def render(self, seed=1, max_depth=4, roughness=0.0, stats=False, tile=16, light_spp=1):
+    def render(self, seed=1, max_depth=4, roughness=0.0, stats=False, tile=16, light_spp=1, progressive_frame=0,
+               accum=None):
+        """Whole frame to host memory.  progressive_frame n >= 1: zone A frame n lerped into
+        `accum` (updated in place and returned)."""
         info = self.scene.info()
-        out = np.zeros((info.res_y, info.res_x, 3), np.float32)
-        p = self.frame_params(seed, max_depth, roughness, tile=tile, stats=stats, light_spp=light_spp)
+        if accum is not None:
+            if accum.dtype != np.float32 or accum.shape != (info.res_y, info.res_x, 3) or not accum.flags.c_contiguous:
+                raise ValueError("accum must be a C-contiguous float32 (res_y, res_x, 3) array")
+            out = accum
+        else:
+            out = np.zeros((info.res_y, info.res_x, 3), np.float32)
+        p = self.frame_params(seed, max_depth, roughness, tile=tile, stats=stats, light_spp=light_spp,
+                              progressive_frame=progressive_frame)
         check(_lib.load().drt_render(self.h, C.byref(p), _fp(out)), self.h, "drt_render")
         return out
 

@@ -42,7 +42,7 @@ class DrtCamera(C.Structure):
 class DrtFrameParams(C.Structure):
     _fields_ = [("seed", C.c_uint32), ("max_depth", C.c_int32), ("roughness", C.c_float), ("shard", C.c_int32),
                 ("n_shards", C.c_int32), ("tile", C.c_int32), ("flags", C.c_int32), ("light_spp", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("progressive_frame", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class DrtFrameStats(C.Structure):
@@ -109,6 +109,8 @@ SIGNATURES = {
     "drt_scene_grid_export": (C.c_int, [_vp, _i64, _i32]),
     "drt_scene_camera_frame": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
     "drt_scene_upload": (C.c_int, [_vp, _vp]),
+    "drt_image_rgb8": (C.c_int, [_vp, C.c_int32, C.c_int32, _vp]),
+    "drt_image_write_png": (C.c_int, [C.c_char_p, _vp, C.c_int32, C.c_int32]),
 }
 
 

@@ -376,6 +376,7 @@ struct Plan {
   ReduceArgs R;
   int tiles_y, n_tiles;
   bool persistent;      // path_persistent (BVH) instead of path_kernel
+  bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
 
@@ -404,12 +405,18 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   F.light_grid = 1;
   while ((F.light_grid + 1) * (F.light_grid + 1) <= F.light_spp) F.light_grid++;
   F.light_inv = 1.0f / (float)F.light_spp;
+  if (p->progressive_frame < 0) DRT_FAIL(c, DRT_E_INVALID, "progressive_frame %d < 0", p->progressive_frame);
+  const int prog = p->progressive_frame;
+  P.skip = prog >= 10000;  // FrameCount == MAX_SAMPLES (main.cpp:39, :537)
   const bool AA = c->spp != 0;                           // main.cpp:1005-1010
   F.dof = (c->cam.aperture != 0.0f && AA) ? 1 : 0;       // main.cpp:1013-1017
   const bool seq = F.dof || p->roughness != 0.0f;
   float scale = 1.0f;
   const bool quad0 = !c->lights.empty() && c->lights[0].type == DRT_LIGHT_QUAD;
-  if (AA) {
+  if (prog > 0) {  // zone A: one jittered sample per pixel whatever spp is (main.cpp:540-572)
+    F.mode = MODE_PROG;
+    F.nsub = 1;
+  } else if (AA) {
     F.n_sqrt = (int)std::sqrt((double)c->spp);
     F.mode = seq ? MODE_SEQ : MODE_AA;
     F.nsub = seq ? 1 : (int)c->spp;
@@ -438,6 +445,7 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   R.scale = scale;
   R.tile = F.tile; R.tiles_x = F.tiles_x; R.shard = F.shard; R.n_shards = F.n_shards; R.n_my_tiles = F.n_my_tiles;
   R.res_x = RX; R.res_y = RY;
+  R.prog_frame = prog;
   return DRT_OK;
 }
 
@@ -445,6 +453,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   Plan P;
   int rc = plan_frame(c, p, P);
   if (rc) return rc;
+  if (P.skip) return DRT_OK;
   SceneArgs S;
   rc = scene_args(c, c->accel, S);
   if (rc) return rc;
@@ -522,8 +531,11 @@ int drt_render(drt_ctx* c, const drt_frame_params* p, float* rgb_out) {
   if (!c || !p || !rgb_out) return DRT_E_INVALID;
   if (p->n_shards > 1) DRT_FAIL(c, DRT_E_INVALID, "drt_render renders whole frames; use drt_render_device for shards");
   const size_t n = (size_t)c->cam.res_x * c->cam.res_y * 3;
+  if (p->progressive_frame >= 10000) return DRT_OK;  // MAX_SAMPLES reached: output untouched
   DRT_HIP(c, hipSetDevice(c->device));
   DRT_HIP(c, c->d_frame.ensure(sizeof(float) * n));
+  if (p->progressive_frame > 1)  // the lerp reads the previous frame
+    DRT_HIP(c, hipMemcpyAsync(c->d_frame.p, rgb_out, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
   int rc = run_frame(c, p, c->d_frame.as<float>(), true, c->stream);
   if (rc) return rc;
   DRT_HIP(c, hipMemcpyAsync(rgb_out, c->d_frame.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));

@@ -586,6 +586,21 @@ __device__ __forceinline__ void flush_stats(const FrameArgs& F, const Counters& 
   }
 }
 
+// Progressive zone A primary ray and light sample (main.cpp:556-571): pixel_sample = (x +
+// rand_double(), y + rand_double()) — the double sum of an int and r/32768 rounded to float is
+// the float sum of the same exact operands — then the lens (DoF), then Vector(rand_float(),
+// rand_float(), 0) whose first draw (right-to-left evaluation) is the y component.
+__device__ __forceinline__ void prog_primary(const SceneArgs& S, const FrameArgs& F, const Item& it, KRng& rng,
+                                             RayP& r, V3& ls) {
+  const float px = (float)it.x + rng.rand_float();
+  const float py = (float)it.y + rng.rand_float();
+  if (F.dof) r = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
+  else r = primary_ray(S, px, py);
+  const float ly = rng.rand_float();
+  const float lx = rng.rand_float();
+  ls = mk(lx, ly, 0.0f);
+}
+
 template <int ACCEL, bool TRI_ONLY, bool STATS, int MODE>
 __global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_stack[];
@@ -631,6 +646,12 @@ __global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) 
             color = add(color, trace_path<ACCEL, TRI_ONLY, STATS, true>(S, F, r, ls, rng, C, tst));
           }
         }
+      } else if (MODE == MODE_PROG) {
+        RayP r;
+        V3 ls;
+        prog_primary(S, F, it, rng, r, ls);
+        if (STATS) C.v[ST_SAMPLES]++;
+        color = trace_path<ACCEL, TRI_ONLY, STATS, true>(S, F, r, ls, rng, C, tst);
       } else if (MODE == MODE_WHITTED_QUAD) {
         const int s = it.sub;
         V3 ls = mk(((float)(s % F.grid_size) + 0.5f) / (float)F.grid_size,
@@ -702,8 +723,8 @@ struct Lane {
   float NdotL, NdotH, hitT;
   uint32_t hitPrim, mat;
   int j;
-  // MODE_SEQ only (dead otherwise): the lane owns a pixel and runs its samples in order on the
-  // pixel's keyed stream — sample index, next rand() call index, pixel key
+  // MODE_SEQ / MODE_PROG only (dead otherwise): the lane owns a pixel and runs its samples in
+  // order on the pixel's keyed stream — sample index, next rand() call index, pixel key
   uint32_t smp, rk, pmix;
 };
 // (Measured alternative, kept out: the shading state in a private per-activation frame array
@@ -922,7 +943,7 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
 template <int MODE>
 __device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 V) {
   V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
-  if (MODE == MODE_SEQ) {
+  if (MODE == MODE_SEQ || MODE == MODE_PROG) {
     KRng rng{F.seed, L.pmix, L.rk};
     R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
     L.rk = rng.k;
@@ -1119,6 +1140,26 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     seq_start_sample<STATS>(S, F, L, C);
     return;
   }
+  if (MODE == MODE_PROG) {  // work item = pixel, one sample (main.cpp:540-572)
+    const Item it = decode_item(F, S.res_x, S.res_y, item, 1);
+    if (!it.valid) {
+      F.samples[item] = make_float4(0.f, 0.f, 0.f, 0.f);
+      L.item = kNoItem;
+      return;
+    }
+    L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+    L.depth = 1;
+    L.fsp = 0;
+    L.ior1 = 1.0f;
+    L.fl = 0u;
+    if (STATS) C.v[ST_SAMPLES]++;
+    KRng rng{F.seed, L.pmix, 0};
+    RayP r;
+    prog_primary(S, F, it, rng, r, L.ls);
+    L.rk = rng.k;
+    start_query<STATS>(S, L, r, false, 0.0f, C);
+    return;
+  }
   const int per_pixel = F.nsub;
   const Item it = decode_item(F, S.res_x, S.res_y, item, per_pixel);
   if (!it.valid) {  // padding of a partial tile
@@ -1243,19 +1284,28 @@ __global__ void __launch_bounds__(256) reduce_kernel(ReduceArgs A) {
     float4 v = s[i];
     r += v.x; g += v.y; b += v.z;
   }
-  r *= A.scale; g *= A.scale; b *= A.scale;
+  float* o;
   if (A.full_frame) {
     const uint32_t k = pidx / per_tile, pix = pidx - k * per_tile;
     const uint32_t t = A.shard + k * A.n_shards;
     const int x = (int)((t % A.tiles_x) * A.tile + pix % A.tile);
     const int y = (int)((t / A.tiles_x) * A.tile + pix / A.tile);
     if (x >= A.res_x || y >= A.res_y) return;
-    float* o = A.out + 3 * ((size_t)y * A.res_x + x);
-    o[0] = r; o[1] = g; o[2] = b;
+    o = A.out + 3 * ((size_t)y * A.res_x + x);
   } else {
-    float* o = A.out + 3 * (size_t)pidx;
-    o[0] = r; o[1] = g; o[2] = b;
+    o = A.out + 3 * (size_t)pidx;
   }
+  if (A.prog_frame > 1) {  // lerp(a, b, t) = a + t * (b - a) in double (maths.h:56), t = 1.0 / FrameCount
+    const double t = 1.0 / (double)A.prog_frame;
+    o[0] = (float)((double)o[0] + t * ((double)r - (double)o[0]));
+    o[1] = (float)((double)o[1] + t * ((double)g - (double)o[1]));
+    o[2] = (float)((double)o[2] + t * ((double)b - (double)o[2]));
+    return;
+  }
+  if (A.prog_frame == 0) {
+    r *= A.scale; g *= A.scale; b *= A.scale;
+  }
+  o[0] = r; o[1] = g; o[2] = b;
 }
 
 // Shard-compact buffers (rank-major, floats_per_shard apart) -> full frame.
@@ -1327,6 +1377,7 @@ static void launch_path_t(const SceneArgs& S, const FrameArgs& F, bool stats, hi
   switch (F.mode) {
     case MODE_AA: launch_path_m<A, T, MODE_AA>(S, F, stats, st); break;
     case MODE_SEQ: launch_path_m<A, T, MODE_SEQ>(S, F, stats, st); break;
+    case MODE_PROG: launch_path_m<A, T, MODE_PROG>(S, F, stats, st); break;
     case MODE_WHITTED_QUAD: launch_path_m<A, T, MODE_WHITTED_QUAD>(S, F, stats, st); break;
     default: launch_path_m<A, T, MODE_WHITTED_POINT>(S, F, stats, st); break;
   }
@@ -1351,9 +1402,7 @@ static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStrea
 template <bool T, bool ST, int M>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
   switch (F.waves) {  // register budget: waves per SIMD the kernel is compiled for
-    case 5: launch_persistent_w<T, ST, M, 5>(S, F, st); break;
     case 7: launch_persistent_w<T, ST, M, 7>(S, F, st); break;
-    case 8: launch_persistent_w<T, ST, M, 8>(S, F, st); break;
     default: launch_persistent_w<T, ST, M, 6>(S, F, st); break;
   }
 }
@@ -1363,6 +1412,7 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
     case MODE_AA: launch_persistent_m<T, ST, MODE_AA>(S, F, st); break;
     case MODE_WHITTED_QUAD: launch_persistent_m<T, ST, MODE_WHITTED_QUAD>(S, F, st); break;
     case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ>(S, F, st); break;
+    case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT>(S, F, st); break;
   }
 }

@@ -13,7 +13,8 @@ enum FrameMode : int {
   MODE_AA = 0,            // one thread per (pixel, sample): main.cpp:618-671 without DoF/roughness
   MODE_SEQ = 1,           // one thread per pixel, samples in order with the keyed RNG stream
   MODE_WHITTED_QUAD = 2,  // one thread per (pixel, regular light sample): main.cpp:683-697
-  MODE_WHITTED_POINT = 3  // one thread per pixel: main.cpp:698-701
+  MODE_WHITTED_POINT = 3,  // one thread per pixel: main.cpp:698-701
+  MODE_PROG = 4            // progressive zone A: one jittered sample per pixel, main.cpp:540-586
 };
 
 enum StatSlot : int {
@@ -84,7 +85,7 @@ struct FrameArgs {
   unsigned int* work_counter;  // persistent kernel: next unclaimed work item (zeroed per frame)
   int refill_min;              // persistent kernel: refill a wave once this many lanes are idle
   int process_min;             // persistent kernel: shade once this many lanes have a result
-  int waves;                   // persistent kernel: register budget (waves per SIMD: 5-8)
+  int waves;                   // persistent kernel: register budget (waves per SIMD: 6 or 7)
 };
 
 struct ReduceArgs {
@@ -94,6 +95,7 @@ struct ReduceArgs {
   int tile, tiles_x, shard, n_shards, n_my_tiles;
   int res_x, res_y;
   int full_frame;  // write the (x, y) frame, else the shard-compact buffer
+  int prog_frame;  // > 0: progressive FrameCount, out = lerp(out, sample, 1/n) (main.cpp:574-586)
   float* out;
 };
 

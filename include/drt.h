@@ -133,7 +133,12 @@ typedef struct {
   int32_t flags;       /* DRT_FRAME_STATS: count rays / node visits / prim tests        */
   int32_t light_spp;   /* extension: shadow samples per quad light per
                           hit, 0 or 1 = the reference (main.cpp:391: one sample)          */
-  int32_t reserved[4];
+  int32_t progressive_frame; /* 0: renderScene zone B.  n >= 1: zone A (main.cpp:536-599) with
+                          FrameCount n — one jittered sample per pixel, written (n = 1) or
+                          lerped into the output with weight 1/n (n > 1: the output buffer is
+                          read, so pass the previous frame back); n >= MAX_SAMPLES (10000)
+                          leaves the output untouched (main.cpp:537)                     */
+  int32_t reserved[3];
 } drt_frame_params;
 
 typedef struct {

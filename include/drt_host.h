@@ -70,6 +70,16 @@ int drt_scene_camera_frame(const drt_scene* s, drt_camera* out);
 
 int drt_scene_upload(drt_ctx* ctx, drt_scene* s);
 
+/* ---- output image ---- */
+/* u8fromfloat (maths.h:126-130: x*255.99f >= 255 ? 255 : (uint8_t)(x*255.99f), negatives -> 0)
+ * of a float RGB frame, out[3*(x + RES_X*y) + c] — the img_Data fill of main.cpp:716-718
+ * without its counter++ race (row 0 = bottom, as the frame). */
+int drt_image_rgb8(const float* rgb, int32_t res_x, int32_t res_y, uint8_t* out);
+/* saveImgFile (main.cpp:251-266) as DevIL writes a lower-left-origin image: an 8-bit RGB PNG
+ * whose first (top) row is the frame's row RES_Y-1.  Returns 0 or DRT_E_INVALID / DRT_E_OOM /
+ * -7 (file error). */
+int drt_image_write_png(const char* path, const float* rgb, int32_t res_x, int32_t res_y);
+
 #ifdef __cplusplus
 }
 #endif

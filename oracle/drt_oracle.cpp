@@ -1368,6 +1368,8 @@ int orc_render(orc_scene* s, uint32_t seed, const orc_options* opt, float* rgb, 
   const uint32_t spp = s->spp;
   const bool AA = spp != 0;                                // main.cpp:1005-1010
   const bool DOF = (s->cam.aperture != 0) && AA;           // main.cpp:1013-1017
+  const long prog = opt ? opt->progressive_frame : 0;      // FrameCount of zone A, 0 = zone B
+  if (prog >= 10000) return 0;                             // FrameCount == MAX_SAMPLES: no render (main.cpp:537)
   int threads = (opt && opt->threads > 0) ? opt->threads : 0;
 #ifdef _OPENMP
   int nthr = threads > 0 ? threads : omp_get_max_threads();
@@ -1386,6 +1388,25 @@ int orc_render(orc_scene* s, uint32_t seed, const orc_options* opt, float* rgb, 
 #endif
     KRng g{seed, (uint32_t)(y * RX + x), 0};
     C3 color = cmk(0, 0, 0);
+    if (prog > 0) {  // zone A (main.cpp:540-586): one jittered sample, lerped into the frame
+      V3 ps;
+      ps.x = (float)((double)x + (double)g.rand_() / ((double)kRandMax + 1.0));  // rand_double (maths.h:88)
+      ps.y = (float)((double)y + (double)g.rand_() / ((double)kRandMax + 1.0));
+      ps.z = 0.0f;
+      Ray ray;
+      if (!DOF) ray = s->cam.primary(ps);
+      else ray = s->cam.primary_lens(dvf(mul(rnd_unit_disk(g), s->cam.aperture), 2.0f), ps);
+      const float ly = g.rand_float();  // Vector(rand_float(), rand_float(), 0.0f): right to left
+      const float lx = g.rand_float();
+      st.samples++;
+      color = s->ray_tracing(ray, 1, 1.0f, mk(lx, ly, 0.0f), g, st);
+      size_t ic = (size_t)3 * ((size_t)x + (size_t)RX * y);
+      const float c3[3] = {color.r, color.g, color.b};
+      for (int k = 0; k < 3; k++)  // lerp(a, b, t) = a + t * (b - a) in double (maths.h:56)
+        rgb[ic + k] = prog == 1 ? c3[k] : (float)((double)rgb[ic + k] + (1.0 / (double)prog) *
+                                                                       ((double)c3[k] - (double)rgb[ic + k]));
+      continue;
+    }
     if (AA) {  // main.cpp:618-671
       int n = (int)std::sqrt((double)spp);
       std::vector<V3> r(spp), sm(spp);

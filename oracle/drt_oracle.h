@@ -61,6 +61,8 @@ typedef struct {
   int threads;      /* OpenMP threads, 0 = all                                     */
   int row_begin, row_end;  /* render only rows [row_begin,row_end) (bounded sample) */
   int light_spp;    /* shadow samples per quad light per hit (C3); 0/1 = reference  */
+  int progressive_frame; /* 0 = zone B; n >= 1 = zone A frame FrameCount n: one sample per
+                            pixel lerped into rgb (in/out) with weight 1/n (main.cpp:536-599) */
 } orc_options;
 
 /* ---- scene construction ---- */

@@ -47,7 +47,8 @@ class OrcStats(C.Structure):
 
 class OrcOptions(C.Structure):
     _fields_ = [("max_depth", C.c_int), ("roughness", C.c_float), ("threads", C.c_int),
-                ("row_begin", C.c_int), ("row_end", C.c_int), ("light_spp", C.c_int)]
+                ("row_begin", C.c_int), ("row_end", C.c_int), ("light_spp", C.c_int),
+                ("progressive_frame", C.c_int)]
 
 
 def build(force: bool = False) -> None:
@@ -317,10 +318,17 @@ class Scene:
         lib().orc_ray_color(self.h, fp(r), fp(ls), len(r), depth, ior, seed, pixel, fp(out))
         return out
 
-    def render(self, seed=1, max_depth=4, roughness=0.0, threads=0, rows=None, light_spp=1):
+    def render(self, seed=1, max_depth=4, roughness=0.0, threads=0, rows=None, light_spp=1, progressive_frame=0,
+               accum=None):
+        """progressive_frame n >= 1: zone A frame n, lerped into `accum` (updated in place)."""
         info = self.info()
-        opt = OrcOptions(max_depth, roughness, threads, rows[0] if rows else 0, rows[1] if rows else 0, light_spp)
-        out = np.zeros((info.res_y, info.res_x, 3), np.float32)
+        opt = OrcOptions(max_depth, roughness, threads, rows[0] if rows else 0, rows[1] if rows else 0, light_spp,
+                         progressive_frame)
+        if accum is not None:
+            assert accum.dtype == np.float32 and accum.shape == (info.res_y, info.res_x, 3) and accum.flags.c_contiguous
+            out = accum
+        else:
+            out = np.zeros((info.res_y, info.res_x, 3), np.float32)
         st = OrcStats()
         rc = lib().orc_render(self.h, seed, C.byref(opt), fp(out), C.byref(st))
         if rc:

@@ -151,6 +151,28 @@ def test_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
     assert st["samples"] == rst["samples"]
 
 
+@pytest.mark.parametrize("accel,aperture,roughness", [("bvh", 0.0, 0.0), ("bvh", 8.0, 0.2), ("grid", 0.0, 0.0),
+                                                     ("none", 8.0, 0.0)])
+def test_progressive_matches_oracle(drt, oracle_mod, renderer, tmp_path, accel, aperture, roughness):
+    """Zone A (main.cpp:536-599): three progressive frames, each lerped into the running buffer."""
+    a, b = load_both(drt, oracle_mod, tmp_path,
+                     sg.mixed_scene_text(res=(24, 16), spp=4, accel=accel, aperture=aperture, focal=1.5, n_tris=60))
+    renderer.upload(a)
+    acc_g = np.zeros((16, 24, 3), np.float32)
+    acc_o = np.zeros((16, 24, 3), np.float32)
+    for n in (1, 2, 3):
+        renderer.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_g, stats=True)
+        st = renderer.stats()
+        _, rst = b.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_o)
+        compare_images(acc_g, acc_o)
+        assert st["samples"] == rst["samples"] == 24 * 16
+        if accel != "none":
+            assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
+    before = acc_g.copy()
+    renderer.render(seed=9, progressive_frame=10000, accum=acc_g)  # MAX_SAMPLES: untouched
+    np.testing.assert_array_equal(acc_g, before)
+
+
 def test_sharded_frame_equals_whole_frame(drt, renderer, tmp_path):
     """Interleaved 16x16 tile shards rendered separately and reassembled == one-shot frame."""
     import torch

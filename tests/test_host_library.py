@@ -141,3 +141,31 @@ def test_p3f_loader_matches_oracle(oracle_mod, scene):
         x, y = a.bvh_export(), b.bvh_export()
         np.testing.assert_array_equal(x["order"], y["order"])
         np.testing.assert_array_equal(bits(x["boxes"]), bits(y["boxes"]))
+
+
+def _u8fromfloat(x):  # maths.h:126-130 in float32
+    v = np.float32(x) * np.float32(255.99)
+    return np.where(v >= 255.0, 255, np.where(v > 0, v, 0)).astype(np.uint8)
+
+
+def test_image_rgb8_is_u8fromfloat():
+    import distributionraytracer_amd as d
+
+    rng = np.random.default_rng(4)
+    f = rng.random((7, 9, 3), dtype=np.float32) * 1.2 - 0.1
+    f[0, 0] = [1.0, 0.99609375, 0.0]
+    np.testing.assert_array_equal(d.image_rgb8(f), _u8fromfloat(f))
+
+
+def test_write_png_is_upright_rgb8(tmp_path):
+    import distributionraytracer_amd as d
+    from PIL import Image
+
+    rng = np.random.default_rng(5)
+    f = rng.random((6, 11, 3), dtype=np.float32)
+    p = tmp_path / "RT_Output.png"
+    d.write_png(p, f)
+    img = np.asarray(Image.open(p))
+    assert img.shape == (6, 11, 3) and img.dtype == np.uint8
+    # lower-left-origin frame: the PNG's top row is the frame's last row (DevIL, main.cpp:251-266)
+    np.testing.assert_array_equal(img, _u8fromfloat(f)[::-1])

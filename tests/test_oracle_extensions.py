@@ -43,3 +43,23 @@ def test_light_spp_multiplies_quad_shadow_rays(oracle_mod, tmp_path):
     assert s4["closest_calls"] == s1["closest_calls"]
     assert s4["shadow_calls"] * 3 == s1["shadow_calls"] * 6
     assert np.isfinite(img4).all() and img4.min() >= 0.0 and img4.max() <= 1.0
+
+
+def test_progressive_frames_average(oracle_mod, tmp_path):
+    """Zone A (main.cpp:536-599): frame n lerps its sample in with weight 1/n, so after n frames
+    the buffer is the running mean of the n one-sample frames (up to float rounding)."""
+    s = _scene(oracle_mod, tmp_path, res=(20, 12), spp=4, accel="bvh")
+    singles = [s.render(seed=100 + n, progressive_frame=1)[0] for n in range(1, 5)]
+    acc = np.zeros_like(singles[0])
+    for n in range(1, 5):
+        s.render(seed=100 + n, progressive_frame=n, accum=acc)
+    np.testing.assert_allclose(acc, np.mean(singles, axis=0), atol=2e-6)
+    # different seeds give different jitter / light samples
+    assert (singles[0] != singles[1]).any()
+
+
+def test_progressive_stops_at_max_samples(oracle_mod, tmp_path):
+    s = _scene(oracle_mod, tmp_path, res=(8, 8), spp=1, accel="bvh")
+    acc = np.full((8, 8, 3), 0.25, np.float32)
+    _, st = s.render(seed=3, progressive_frame=10000, accum=acc)
+    assert (acc == 0.25).all() and st["samples"] == 0
