@@ -46,12 +46,12 @@ def synthetic_triangles(n, seed=1):
     return np.concatenate([v.astype(np.float32).reshape(n, 9), FLOOR])
 
 
-def populate(scene, tris, res, spp, aperture=0.0, focal=1.0):
+def populate(scene, tris, res, spp, aperture=0.0, focal=1.0, accel="bvh"):
     """Same calls for the product scene and the oracle scene (P3F-equivalent content)."""
     scene.set_camera(CAMERA["eye"], CAMERA["at"], CAMERA["up"], CAMERA["fovy"], CAMERA["hither"], res, res,
                      aperture, focal)
     scene.set_background((0.078, 0.361, 0.753))
-    scene.set_accel("bvh")
+    scene.set_accel(accel)
     scene.set_spp(spp)
     scene.add_light_quad((4, 3, 2), (1, 1, 1), (4, 2, 2), (3, 3, 2), 16)
     scene.add_light_point((-3, 1, 5), (1, 1, 1))
@@ -66,7 +66,7 @@ def cpu_baseline(tris, res, spp, seed, target_s, threads, ext):
 
     O.build()
     s = O.Scene.new()
-    populate(s, tris, res, spp, ext["aperture"], ext["focal"])
+    populate(s, tris, res, spp, ext["aperture"], ext["focal"], ext["accel"])
     kw = {k: ext[k] for k in ("max_depth", "roughness", "light_spp")}
     t0 = time.time()
     s.build()
@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--roughness", type=float, default=0.0, help="glossy reflection (C4: 0.1)")
     ap.add_argument("--max-depth", type=int, default=4, help="MAX_DEPTH (C4: 8)")
     ap.add_argument("--light-spp", type=int, default=1, help="shadow samples per quad light (C3: 4)")
+    ap.add_argument("--accel", default="bvh", choices=["bvh", "grid", "none"], help="accelerator (scene.h:22)")
+    ap.add_argument("--check-frame", action="store_true",
+                    help="after timing, rank 0 checks the assembled frame against a whole-frame render (bitwise)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
@@ -120,9 +123,16 @@ def main():
     import distributionraytracer_amd as drt
     from distributionraytracer_amd.sharding import FrameGather, TileLayout
 
-    torch.cuda.set_device(local)
+    # one process per GPU; DRT_DIST_BACKEND=gloo (with ranks folded onto the visible devices) only
+    # rehearses the multi-rank script path on a box with fewer GPUs than ranks
+    backend = os.environ.get("DRT_DIST_BACKEND", "nccl")
+    dev = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     def log(*a):
         if rank == 0:
@@ -132,14 +142,14 @@ def main():
     tris = synthetic_triangles(args.tris, args.seed)
     scene = drt.Scene()
     ext = {"aperture": args.aperture, "focal": args.focal, "roughness": args.roughness,
-           "max_depth": args.max_depth, "light_spp": args.light_spp}
-    populate(scene, tris, args.res, args.spp, args.aperture, args.focal)
+           "max_depth": args.max_depth, "light_spp": args.light_spp, "accel": args.accel}
+    populate(scene, tris, args.res, args.spp, args.aperture, args.focal, args.accel)
     scene.build()
     info = scene.info()
     build_s = time.time() - t0
     log(f"[bench] scene: {info.n_objects} objects, BVH {info.bvh_nodes} nodes, host build {info.build_ms / 1e3:.2f} s "
         f"(total setup {build_s:.1f} s)")
-    r = drt.Renderer(local)
+    r = drt.Renderer(dev)
     r.upload(scene)
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
@@ -199,6 +209,17 @@ def main():
     dt = float(dt_t.item())
 
     path_ms, total_ms = r.frame_times(args.steps)
+    frame_check = None
+    if args.check_frame:
+        step(shard_p)  # assemble one more frame, then compare it with a one-shot whole frame
+        torch.cuda.synchronize()
+        if rank == 0:
+            whole = torch.empty_like(frame)
+            r.render_device(r.frame_params(seed=args.seed, **fkw), whole.data_ptr(), sptr)
+            torch.cuda.synchronize()
+            frame_check = bool(torch.equal(whole.view(torch.int32), frame.view(torch.int32)))
+        if world > 1:
+            dist.barrier()
     host_frame_ms = None
     if world == 1:
         # PCIe-inclusive variant (not `value`): drt_render with the frame copied to host memory
@@ -210,8 +231,8 @@ def main():
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    extras = [f"{k}{v:g}" for k, v in ext.items()
-              if v != {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1}[k]]
+    dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh"}
+    extras = [f"{k}{v if isinstance(v, str) else format(v, 'g')}" for k, v in ext.items() if v != dflt[k]]
     workload_key = "_".join([f"tris{args.tris}_res{args.res}_spp{args.spp}"] + extras)
     tj = Path(args.traffic_json)
     if world == 1 and tj.exists():
@@ -236,18 +257,19 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded random triangle soup, SURVEY.md §8d)",
-        "config": {"workload": f"synthetic {args.tris} triangles + floor, BVH, {args.res}x{args.res}, "
+        "config": {"workload": f"synthetic {args.tris} triangles + floor, {args.accel.upper()}, {args.res}x{args.res}, "
                                f"{args.spp} spp, MAX_DEPTH {args.max_depth}, 1 quad + 1 point light"
                                + (f", DoF aperture {args.aperture:g} focal {args.focal:g}" if args.aperture else "")
                                + (f", roughness {args.roughness:g}" if args.roughness else "")
                                + (f", {args.light_spp} quad-light samples" if args.light_spp > 1 else ""),
-                   "tris": args.tris, "res": args.res, "spp": args.spp, "accel": "bvh", "key": workload_key,
+                   "tris": args.tris, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
                    "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "path_kernel<BVH,tri>", "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3)},
         "host_output_frame_ms": None if host_frame_ms is None else round(host_frame_ms, 3),
+        **({"frame_check_vs_whole_frame": frame_check} if args.check_frame else {}),
         "rays_per_frame": int(rays_frame),
         "samples_per_frame": int(tot["samples"]),
         "msamples_per_s": round(tot["samples"] * args.steps / dt / 1e6, 2),
