@@ -46,7 +46,7 @@ def synthetic_triangles(n, seed=1):
     return np.concatenate([v.astype(np.float32).reshape(n, 9), FLOOR])
 
 
-def populate(scene, tris, res, spp, aperture=0.0, focal=1.0, accel="bvh"):
+def populate(scene, tris, res, spp, aperture=0.0, focal=1.0, accel="bvh", ks=0.5):
     """Same calls for the product scene and the oracle scene (P3F-equivalent content)."""
     scene.set_camera(CAMERA["eye"], CAMERA["at"], CAMERA["up"], CAMERA["fovy"], CAMERA["hither"], res, res,
                      aperture, focal)
@@ -55,7 +55,7 @@ def populate(scene, tris, res, spp, aperture=0.0, focal=1.0, accel="bvh"):
     scene.set_spp(spp)
     scene.add_light_quad((4, 3, 2), (1, 1, 1), (4, 2, 2), (3, 3, 2), 16)
     scene.add_light_point((-3, 1, 5), (1, 1, 1))
-    scene.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), 0.5, 30.0827, 0, 1)
+    scene.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), ks, 30.0827, 0, 1)
     scene.add_triangles(tris)
 
 
@@ -66,7 +66,7 @@ def cpu_baseline(tris, res, spp, seed, target_s, threads, ext):
 
     O.build()
     s = O.Scene.new()
-    populate(s, tris, res, spp, ext["aperture"], ext["focal"], ext["accel"])
+    populate(s, tris, res, spp, ext["aperture"], ext["focal"], ext["accel"], ext["ks"])
     kw = {k: ext[k] for k in ("max_depth", "roughness", "light_spp")}
     t0 = time.time()
     s.build()
@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--max-depth", type=int, default=4, help="MAX_DEPTH (C4: 8)")
     ap.add_argument("--light-spp", type=int, default=1, help="shadow samples per quad light (C3: 4)")
     ap.add_argument("--accel", default="bvh", choices=["bvh", "grid", "none"], help="accelerator (scene.h:22)")
+    ap.add_argument("--ks", type=float, default=0.5, help="material Ks (0: no mirror bounces; diagnostics)")
     ap.add_argument("--check-frame", action="store_true",
                     help="after timing, rank 0 checks the assembled frame against a whole-frame render (bitwise)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -142,8 +143,8 @@ def main():
     tris = synthetic_triangles(args.tris, args.seed)
     scene = drt.Scene()
     ext = {"aperture": args.aperture, "focal": args.focal, "roughness": args.roughness,
-           "max_depth": args.max_depth, "light_spp": args.light_spp, "accel": args.accel}
-    populate(scene, tris, args.res, args.spp, args.aperture, args.focal, args.accel)
+           "max_depth": args.max_depth, "light_spp": args.light_spp, "accel": args.accel, "ks": args.ks}
+    populate(scene, tris, args.res, args.spp, args.aperture, args.focal, args.accel, args.ks)
     scene.build()
     info = scene.info()
     build_s = time.time() - t0
@@ -231,7 +232,7 @@ def main():
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh"}
+    dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh", "ks": 0.5}
     extras = [f"{k}{v if isinstance(v, str) else format(v, 'g')}" for k, v in ext.items() if v != dflt[k]]
     workload_key = "_".join([f"tris{args.tris}_res{args.res}_spp{args.spp}"] + extras)
     tj = Path(args.traffic_json)
@@ -293,6 +294,10 @@ def main():
         # share of the node section spent in the leaf (primitive test) block
         "leaf_share_of_node": round(tot["cycles_leaf"] / max(1.0, tot["cycles_node"]), 3),
         "leaf_iter_frac": round(tot["wave_leaf_iters"] / max(1.0, tot["wave_node_iters"]), 3),
+        # s_memtime cycles per wave-level iteration (stats frame; stamps cost some cycles themselves)
+        "cycles_per_iter": {"node": round(tot["cycles_node"] / max(1.0, tot["wave_node_iters"]), 1),
+                            "leaf_block": round(tot["cycles_leaf"] / max(1.0, tot["wave_leaf_iters"]), 1),
+                            "shade": round(tot["cycles_shade"] / max(1.0, tot["wave_path_iters"]), 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

@@ -202,7 +202,10 @@ int drt_upload_scene(drt_ctx* c, const drt_scene_desc* s) {
   if (s->n_lights > 0 && !c->lights.empty())
     for (auto& l : c->lights)
       if (l.type != DRT_LIGHT_POINT && l.type != DRT_LIGHT_QUAD) DRT_FAIL(c, DRT_E_INVALID, "bad light type");
-  DRT_HIP(c, c->d_prims.ensure(sizeof(PrimRecord) * c->prims_scene.size()));
+  // + 64 B: the BVH node step reads four 16-B slots from a leaf's first record and, for leaves of
+  // two or more, two more; the tail slots of the last record must stay inside the allocation
+  DRT_HIP(c, c->d_prims.ensure(sizeof(PrimRecord) * c->prims_scene.size() + kPrimPadBytes));
+  DRT_HIP(c, hipMemset(c->d_prims.p, 0, sizeof(PrimRecord) * c->prims_scene.size() + kPrimPadBytes));
   DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
                        hipMemcpyHostToDevice));
   DRT_HIP(c, c->d_lights.ensure(sizeof(drt_light) * std::max<size_t>(1, c->lights.size())));

@@ -786,8 +786,14 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // node — make ONE pop attempt.  A closest-hit pop that is pruned (t >= best, bvh.cpp:303) leaves
 // LF_POP set, so the next iteration tries the next entry; the visit order is exactly the
 // reference's, only spread over iterations with uniform, short control flow.
-// (Measured alternative, kept out: one primitive per iteration with a fetch shared by node and
-// leaf lanes — fewer leaf-block cycles but more iterations, 3 % slower overall.)
+//
+// Memory: a lane visits either an inner node or a leaf, so one fetch serves both kinds of lanes.
+// Every visiting lane loads four 16-B slots of its record (the 64-B node record, or the leaf's
+// first 48-B primitive record plus the first slot of the second) and leaves of two or more
+// primitives two more slots; then the wave waits ONCE and each lane computes on the same
+// registers.  Without this a wave with lanes of both kinds paid two dependent round trips per
+// iteration.  Primitives past the second (SAH leaves, bvh.cpp:193) are fetched in pairs after.
+// (Measured alternative, kept out: one primitive per iteration — more iterations, 3 % slower.)
 template <bool TRI_ONLY, bool STATS, int CAP>
 __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
@@ -796,13 +802,30 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
   const bool shadow = (fl & LF_SHADOW) != 0u;
   const uint32_t cur = L.cur;
   const bool visit = !(fl & LF_POP);
-  // the inner-node and leaf visits are two consecutive exec-masked blocks (as compiled anyway);
-  // stats builds time the leaf block
-  if (visit && !desc_is_leaf(cur)) {
+  const bool inner = visit && !desc_is_leaf(cur);
+  const bool leaf = visit && desc_is_leaf(cur);
+  uint32_t first = desc_first(cur), cnt = desc_count(cur);
+  if (leaf && cnt == kBigLeaf) {  // oversized leaf: (first, count) from the side table
+    const uint2 bl = S.big_leaves[first];
+    first = bl.x;
+    cnt = bl.y;
+  }
+  const float4* rec = leaf ? S.prims + 3 * (size_t)first : S.nodes + 4 * (size_t)cur;
+  float4 s0, s1, s2, s3, s4, s5;
+  if (visit) {
+    s0 = rec[0];
+    s1 = rec[1];
+    s2 = rec[2];
+    s3 = rec[3];
+  }
+  if (leaf && cnt > 1) {
+    s4 = rec[4];
+    s5 = rec[5];
+  }
+  if (inner) {
     if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
-    const float4* nd = S.nodes + 4 * (size_t)cur;
-    const float4 a = nd[0], b = nd[1], c = nd[2];
-    const uint4 d = *reinterpret_cast<const uint4*>(nd + 3);
+    const float4 a = s0, b = s1, c = s2;
+    const uint4 d = make_uint4(__float_as_uint(s3.x), __float_as_uint(s3.y), 0u, 0u);
     float tL, tR;
     bool hL, hR;
     if (wave_finite) {
@@ -840,7 +863,6 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
       if (spa >= kLdsBytes) C.v[ST_PUSH_SPILL]++;
     }
   }
-  const bool leaf = visit && desc_is_leaf(cur);
   uint64_t t0 = 0;
   if (STATS) {
     t0 = stamp_cycles();
@@ -848,16 +870,28 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
   }
   if (leaf) {
     if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
-    uint32_t first = desc_first(cur), cnt = desc_count(cur);
-    if (cnt == kBigLeaf) {
-      const uint2 bl = S.big_leaves[first];
-      first = bl.x;
-      cnt = bl.y;
-    }
-    // primitives in pairs: both records are fetched before the first test, so a two-primitive
-    // leaf costs one memory round trip; tests (and the shadow early exit) stay in order
+    bool done = false;  // shadow any-hit found (bvh.cpp:376-377)
+    // leaf_test: one Object::hit of the leaf in order (bvh.cpp:287-295 / :370-378)
+    auto leaf_test = [&](const float4& p0, const float4& p1, const float4& p2, uint32_t prim) {
+      if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+      float t;
+      if (hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t)) {
+        if (shadow) {
+          if (t <= L.thr) {
+            fl = (fl | LF_HIT) & ~LF_TRAV;
+            done = true;
+          }
+        } else if (t < L.best_t) {
+          L.best_t = t;
+          L.best_prim = prim;
+          fl |= LF_HIT;
+        }
+      }
+    };
+    if (cnt > 0) leaf_test(s0, s1, s2, first);
+    if (!done && cnt > 1) leaf_test(s3, s4, s5, first + 1);
     const float4* pr = S.prims + 3 * (size_t)first;
-    for (uint32_t i = 0; i < cnt; i += 2) {
+    for (uint32_t i = 2; !done && i < cnt; i += 2) {  // primitives in pairs, tested in order
       const bool two = i + 1 < cnt;
       const float4 p0 = pr[3 * i], p1 = pr[3 * i + 1], p2 = pr[3 * i + 2];
       float4 r0, r1, r2;
@@ -866,34 +900,8 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
         r1 = pr[3 * i + 4];
         r2 = pr[3 * i + 5];
       }
-      if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
-      float t;
-      if (hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t)) {
-        if (shadow) {
-          if (t <= L.thr) {  // any-hit: done (bvh.cpp:376-377)
-            fl = (fl | LF_HIT) & ~LF_TRAV;
-            break;
-          }
-        } else if (t < L.best_t) {
-          L.best_t = t;
-          L.best_prim = first + i;
-          fl |= LF_HIT;
-        }
-      }
-      if (!two) break;
-      if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
-      if (hit_prim_rec<TRI_ONLY>(r0, r1, r2, L.q, t)) {
-        if (shadow) {
-          if (t <= L.thr) {
-            fl = (fl | LF_HIT) & ~LF_TRAV;
-            break;
-          }
-        } else if (t < L.best_t) {
-          L.best_t = t;
-          L.best_prim = first + i + 1;
-          fl |= LF_HIT;
-        }
-      }
+      leaf_test(p0, p1, p2, first + i);
+      if (!done && two) leaf_test(r0, r1, r2, first + i + 1);
     }
     if (fl & LF_TRAV) fl |= LF_POP;
   }

@@ -35,6 +35,7 @@ constexpr int kMaxFrames = 16;     // max_depth <= 15
 constexpr int kMaxBvhDepth = 96;   // traversal stack entries (host rejects deeper trees)
 constexpr int kLdsStack = 16;      // traversal stack entries kept in LDS per thread
 constexpr int kBlock = 256;        // path-kernel block size
+constexpr size_t kPrimPadBytes = 64;  // zeroed tail of the primitive buffer (node_step's slot reads)
 
 struct SceneArgs {
   // Camera (camera.h:32-61), precomputed on the host
