@@ -224,6 +224,7 @@ def main():
     host_frame_ms = None
     if world == 1:
         # PCIe-inclusive variant (not `value`): drt_render with the frame copied to host memory
+        r.render(seed=args.seed, **fkw)  # first call allocates the context's host-path buffers
         t_h = time.perf_counter()
         r.render(seed=args.seed, **fkw)
         host_frame_ms = (time.perf_counter() - t_h) * 1e3
