@@ -17,8 +17,9 @@ void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_onl
 void launch_reduce(const ReduceArgs& A, hipStream_t st);
 void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, int n_tiles, int n_shards,
                     int tiles_per_shard, int res_x, int res_y, hipStream_t st);
-bool persistent_supported(int accel, int mode);
-void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, bool tri_only, bool stats, hipStream_t st);
+bool persistent_supported(int accel, const int gdim[3]);
+void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats,
+                            hipStream_t st);
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
                   float* nrm, int32_t* obj, uint8_t* occ, hipStream_t st);
 }  // namespace drt
@@ -434,7 +435,7 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
     F.mode = seq ? MODE_SEQ : MODE_WHITTED_POINT;
     F.nsub = 1;
   }
-  P.persistent = persistent_supported(c->accel, F.mode) && env_int("DRT_PERSISTENT", 1) != 0;
+  P.persistent = persistent_supported(c->accel, c->gdim) && env_int("DRT_PERSISTENT", 1) != 0;
   const int per_pixel = F.mode == MODE_SEQ ? 1 : F.nsub;  // work items per pixel
   int slots = per_pixel;                                   // sample slots per pixel
   if (P.persistent && F.mode == MODE_SEQ) {  // a lane runs a pixel's samples in order, one slot each
@@ -484,7 +485,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     P.F.waves = env_int("DRT_WAVES", 6);
   }
   if (P.F.n_items) {
-    if (persistent) launch_path_persistent(S, P.F, c->tri_only, stats, st);
+    if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
     else launch_path(S, P.F, c->accel, c->tri_only, stats, st);
   }
   DRT_HIP(c, hipGetLastError());

@@ -726,6 +726,9 @@ struct Lane {
   // MODE_SEQ / MODE_PROG only (dead otherwise): the lane owns a pixel and runs its samples in
   // order on the pixel's keyed stream — sample index, next rand() call index, pixel key
   uint32_t smp, rk, pmix;
+  // ACC_GRID only (dead otherwise): the 3D-DDA of Grid::Traverse in double (grid.cpp:200-245);
+  // the cell is packed in `cur` (ix | iy << 10 | iz << 20)
+  double gtx, gty, gtz, gdx, gdy, gdz;
 };
 // (Measured alternative, kept out: the shading state in a private per-activation frame array
 // instead of registers — the extra scratch stores sit in vmcnt ahead of the next node fetch,
@@ -759,14 +762,107 @@ __device__ __forceinline__ bool ray_finite(const RayP& r) {
          fabsf(r.o.z) < __builtin_inff();
 }
 
-template <bool STATS>
+// Grid::Init_Traverse (grid.cpp:160-245) for the lane's query: grid-box entry, first cell and
+// the double-precision DDA state, exactly as grid_traverse computes them.  False: box missed.
+__device__ __forceinline__ bool grid_init(const SceneArgs& S, Lane& L) {
+  const RayP& r = L.q;
+  const int nx = S.gdim[0], ny = S.gdim[1], nz = S.gdim[2];
+  const float x0 = S.gmin[0], y0 = S.gmin[1], z0 = S.gmin[2], x1 = S.gmax[0], y1 = S.gmax[1], z1 = S.gmax[2];
+  const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+  float txmin, tymin, tzmin, txmax, tymax, tzmax;
+  if (r.sx()) { txmin = (x0 - ox) * r.ix; txmax = (x1 - ox) * r.ix; } else { txmin = (x1 - ox) * r.ix; txmax = (x0 - ox) * r.ix; }
+  if (r.sy()) { tymin = (y0 - oy) * r.iy; tymax = (y1 - oy) * r.iy; } else { tymin = (y1 - oy) * r.iy; tymax = (y0 - oy) * r.iy; }
+  if (r.sz()) { tzmin = (z0 - oz) * r.iz; tzmax = (z1 - oz) * r.iz; } else { tzmin = (z1 - oz) * r.iz; tzmax = (z0 - oz) * r.iz; }
+  float t0 = (txmin > tymin) ? txmin : tymin;
+  if (tzmin > t0) t0 = tzmin;
+  float t1 = (txmax < tymax) ? txmax : tymax;
+  if (tzmax < t1) t1 = tzmax;
+  if (t0 > t1 || t1 < 0.0f) return false;  // grid.cpp:170
+  int ix, iy, iz;
+  if (box_inside(x0, y0, z0, x1, y1, z1, r.o)) {
+    ix = dclampi((ox - x0) * nx / (x1 - x0), nx - 1);
+    iy = dclampi((oy - y0) * ny / (y1 - y0), ny - 1);
+    iz = dclampi((oz - z0) * nz / (z1 - z0), nz - 1);
+  } else {
+    V3 p = add(r.o, mul(r.d, t0));
+    ix = dclampi((p.x - x0) * nx / (x1 - x0), nx - 1);
+    iy = dclampi((p.y - y0) * ny / (y1 - y0), ny - 1);
+    iz = dclampi((p.z - z0) * nz / (z1 - z0), nz - 1);
+  }
+  L.gdx = (double)((txmax - txmin) / (float)nx);
+  L.gdy = (double)((tymax - tymin) / (float)ny);
+  L.gdz = (double)((tzmax - tzmin) / (float)nz);
+  L.gtx = (dx > 0.0f) ? (double)txmin + (ix + 1) * L.gdx : (double)txmin + (nx - ix) * L.gdx;
+  if (dx == 0.0f) L.gtx = 3.4028234663852886e38;
+  L.gty = (dy > 0.0f) ? (double)tymin + (iy + 1) * L.gdy : (double)tymin + (ny - iy) * L.gdy;
+  if (dy == 0.0f) L.gty = 3.4028234663852886e38;
+  L.gtz = (dz > 0.0f) ? (double)tzmin + (iz + 1) * L.gdz : (double)tzmin + (nz - iz) * L.gdz;
+  if (dz == 0.0f) L.gtz = 3.4028234663852886e38;
+  L.cur = (uint32_t)ix | ((uint32_t)iy << 10) | ((uint32_t)iz << 20);
+  return true;
+}
+
+// One cell of Grid::Traverse (grid.cpp:247-306 closest, :309-358 shadow): the cell's objects in
+// insertion order (shadow: any t < |d| ends the query), then the DDA step — closest hits end
+// when best.t < t_next of the stepped axis, leaving the grid is a miss (even with a farther hit).
+template <bool TRI_ONLY, bool STATS>
+__device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters& C) {
+  uint32_t fl = L.fl;
+  const bool shadow = (fl & LF_SHADOW) != 0u;
+  const int nx = S.gdim[0], ny = S.gdim[1], nz = S.gdim[2];
+  int ix = (int)(L.cur & 1023u), iy = (int)((L.cur >> 10) & 1023u), iz = (int)(L.cur >> 20);
+  if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
+  const size_t cidx = (size_t)ix + (size_t)nx * iy + (size_t)nx * ny * iz;
+  const uint32_t b = S.cell_start[cidx], e = S.cell_start[cidx + 1];
+  for (uint32_t q = b; q < e; q++) {
+    if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+    const uint32_t obj = S.cell_objs[q];
+    float t;
+    if (hit_prim<TRI_ONLY>(S.prims, obj, L.q, t)) {
+      if (shadow) {
+        if (t < L.thr) {
+          L.fl = (fl | LF_HIT) & ~LF_TRAV;
+          return;
+        }
+      } else if (t < L.best_t) {
+        L.best_t = t;
+        L.best_prim = obj;
+      }
+    }
+  }
+  const float dx = L.q.d.x, dy = L.q.d.y, dz = L.q.d.z;
+  bool end = false, exited = false;
+  if (L.gtx < L.gty && L.gtx < L.gtz) {
+    if (!shadow && (double)L.best_t < L.gtx) end = true;
+    else { L.gtx += L.gdx; ix += (dx > 0.0f) ? 1 : -1; exited = ix == ((dx > 0.0f) ? nx : -1); }
+  } else if (L.gty < L.gtz) {
+    if (!shadow && (double)L.best_t < L.gty) end = true;
+    else { L.gty += L.gdy; iy += (dy > 0.0f) ? 1 : -1; exited = iy == ((dy > 0.0f) ? ny : -1); }
+  } else {
+    if (!shadow && (double)L.best_t < L.gtz) end = true;
+    else { L.gtz += L.gdz; iz += (dz > 0.0f) ? 1 : -1; exited = iz == ((dz > 0.0f) ? nz : -1); }
+  }
+  if (end) fl = (fl & ~LF_TRAV) | (L.best_prim != 0xFFFFFFFFu ? LF_HIT : 0u);
+  else if (exited) fl &= ~LF_TRAV;
+  else L.cur = (uint32_t)ix | ((uint32_t)iy << 10) | ((uint32_t)iz << 20);
+  L.fl = fl;
+}
+
+template <bool STATS, int ACC>
 __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const RayP& q, bool shadow, float thr,
                                             Counters& C) {
   if (STATS) C.v[shadow ? ST_SHADOW : ST_CLOSEST]++;
   L.q = q;
   L.thr = thr;
-  L.spa &= 1023u;
   L.best_t = 3.402823466e+38f;
+  if (ACC == ACC_GRID) {
+    L.best_prim = 0xFFFFFFFFu;
+    const bool in = grid_init(S, L);
+    // a shadow ray that misses the grid box counts as shadowed (grid.cpp:323-324, Q8)
+    L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (in ? LF_TRAV : (shadow ? LF_HIT : 0u));
+    return;
+  }
+  L.spa &= 1023u;
   L.cur = S.root_desc;
   float tmp;
   const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
@@ -930,7 +1026,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
   L.fl = fl;
 }
 
-template <bool STATS>
+template <bool STATS, int ACC>
 __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs& F, Lane& L,
                                              Counters& C) {  // main.cpp:386-422
   const int li = light_of_pair(L.j, F);
@@ -941,9 +1037,11 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
   const V3 H = normalize(add(Lv, L.V));
   L.NdotL = smax(dot(L.N, Lv), 0.0f);
   L.NdotH = smax(dot(L.N, H), 0.0f);
-  // BVH::Traverse(Ray&) normalises Ls and accepts t <= |Ls| + EPSILON (bvh.cpp:321-322, :376)
-  start_query<STATS>(S, L, make_ray(add(L.hitP, mul(L.N, 1e-4f)), normalize(Ls)), true, shadow_threshold(length(Ls)),
-                     C);
+  const V3 so = add(L.hitP, mul(L.N, 1e-4f));
+  if (ACC == ACC_GRID)  // Grid::Traverse(Ray&) gets the unit L: range |L|, direction re-normalised (Q1)
+    start_query<STATS, ACC>(S, L, make_ray(so, normalize(Lv)), true, length(Lv), C);
+  else  // BVH::Traverse(Ray&) normalises Ls and accepts t <= |Ls| + EPSILON (bvh.cpp:321-322, :376)
+    start_query<STATS, ACC>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
 }
 
 // reflectDir (main.cpp:504-508); MODE_SEQ draws rnd_unit_sphere on the lane's keyed stream
@@ -960,11 +1058,11 @@ __device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 
   return normalize(R);
 }
 
-template <bool STATS>
+template <bool STATS, int ACC>
 __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C);
 
 // Consume the completed query of lane L (main.cpp:294-521 between two traversals).
-template <bool STATS, int MODE>
+template <bool STATS, int MODE, int ACC>
 __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Frame* fr, Counters& C) {
   const float offset = 1e-4f;
   V3 c = mk(0, 0, 0);
@@ -987,7 +1085,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       L.lightPos = mk(0, 0, 0);
       L.j = 0;
       if (S.n_lights > 0) {
-        setup_shadow<STATS>(S, F, L, C);
+        setup_shadow<STATS, ACC>(S, F, L, C);
         return;
       }
       after_lights = true;
@@ -996,7 +1094,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
     if (!hit) L.acc = add(L.acc, light_term(S.mats[L.mat], L.NdotL, L.NdotH, S.lights[light_of_pair(L.j, F)], F));
     L.j = next_light_pair(S, F, L.j);
     if (L.j < S.n_lights * F.light_spp) {
-      setup_shadow<STATS>(S, F, L, C);
+      setup_shadow<STATS, ACC>(S, F, L, C);
       return;
     }
     after_lights = true;
@@ -1052,7 +1150,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         L.ior1 = child_ior;
         L.ls = L.lightPos;
         L.depth++;
-        start_query<STATS>(S, L, child, false, 0.0f, C);
+        start_query<STATS, ACC>(S, L, child, false, 0.0f, C);
         return;
       }
       c = cclamp(L.acc);
@@ -1072,7 +1170,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         L.ior1 = f.ior1;
         L.ls = f.lightPos;
         L.depth = L.fsp + 1;
-        start_query<STATS>(S, L, make_ray(add(f.hitP, mul(f.N, offset)), R), false, 0.0f, C);
+        start_query<STATS, ACC>(S, L, make_ray(add(f.hitP, mul(f.N, offset)), R), false, 0.0f, C);
         return;
       }
       c = cclamp(f.acc);
@@ -1087,7 +1185,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
   if (MODE == MODE_SEQ) {  // sample smp of the lane's pixel is done: next sample, same stream
     F.samples[(size_t)L.item * F.nsub + L.smp] = make_float4(c.x, c.y, c.z, 0.0f);
     if (++L.smp < (uint32_t)F.nsub) {
-      seq_start_sample<STATS>(S, F, L, C);
+      seq_start_sample<STATS, ACC>(S, F, L, C);
       return;
     }
     L.item = kNoItem;
@@ -1100,7 +1198,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
 // MODE_SEQ: start sample L.smp of pixel L.item (path_kernel's in-order loop, main.cpp:651-665,
 // or the Whitted light-sample loop with glossy reflection, main.cpp:683-697).  The samples of
 // a pixel go to samples[pixel * nsub + smp]; the ordered reduce sums them as the loop did.
-template <bool STATS>
+template <bool STATS, int ACC>
 __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
   const Item it = decode_item(F, S.res_x, S.res_y, L.item, 1);
   L.depth = 1;
@@ -1128,10 +1226,10 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
                            ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
                       : mk(0.5f, 0.5f, 0.0f);
   }
-  start_query<STATS>(S, L, r, false, 0.0f, C);
+  start_query<STATS, ACC>(S, L, r, false, 0.0f, C);
 }
 
-template <bool STATS, int MODE>
+template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item,
                                           Counters& C) {
   L.item = item;
@@ -1145,7 +1243,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     L.smp = 0;
     L.rk = F.spp > 0 ? 5u * F.spp - 1u : 0u;  // after the prologue's 4 spp + spp - 1 calls
-    seq_start_sample<STATS>(S, F, L, C);
+    seq_start_sample<STATS, ACC>(S, F, L, C);
     return;
   }
   if (MODE == MODE_PROG) {  // work item = pixel, one sample (main.cpp:540-572)
@@ -1165,7 +1263,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     RayP r;
     prog_primary(S, F, it, rng, r, L.ls);
     L.rk = rng.k;
-    start_query<STATS>(S, L, r, false, 0.0f, C);
+    start_query<STATS, ACC>(S, L, r, false, 0.0f, C);
     return;
   }
   const int per_pixel = F.nsub;
@@ -1196,10 +1294,10 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     L.ls = mk(0.5f, 0.5f, 0.0f);
     r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
   }
-  start_query<STATS>(S, L, r, false, 0.0f, C);
+  start_query<STATS, ACC>(S, L, r, false, 0.0f, C);
 }
 
-template <bool TRI_ONLY, bool STATS, int MODE, int WAVES>
+template <bool TRI_ONLY, bool STATS, int MODE, int WAVES, int ACC>
 __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, FrameArgs F) {
   constexpr int CAP = lds_cap(WAVES);
   static_assert(kBlock * 4 == 1024, "spa encoding assumes 256-thread blocks");
@@ -1237,7 +1335,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
       if (L.item == kNoItem) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         const uint32_t it = base + rank;
-        if (it < n_items) lane_init<STATS, MODE>(S, F, L, it, C);
+        if (it < n_items) lane_init<STATS, MODE, ACC>(S, F, L, it, C);
       }
     }
     const bool live = L.item != kNoItem;
@@ -1252,8 +1350,12 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
     // ---- one node step for every lane with a query in flight
     if (trav) {
       if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
-      const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
-      if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
+      if (ACC == ACC_GRID) {
+        if (in_trav) grid_step<TRI_ONLY, STATS>(S, L, C);
+      } else {
+        const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
+        if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
+      }
     }
     const uint64_t t2 = stamp();
     // ---- batched shading for lanes whose query completed
@@ -1263,7 +1365,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
         if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
         if (done) C.v[ST_LANE_PATH_ITERS]++;
       }
-      if (done) lane_process<STATS, MODE>(S, F, L, fr, C);
+      if (done) lane_process<STATS, MODE, ACC>(S, F, L, fr, C);
     }
     if (STATS) {
       const uint64_t t3 = stamp();
@@ -1391,45 +1493,53 @@ static void launch_path_t(const SceneArgs& S, const FrameArgs& F, bool stats, hi
   }
 }
 
-template <bool T, bool ST, int M, int W>
+template <bool T, bool ST, int M, int W, int A>
 static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
+  // the BVH kernel keeps its traversal stack's top in LDS; the Grid stepper needs none
+  const size_t lds = A == ACC_BVH ? (size_t)lds_cap(W) * kBlock * 8 : 0;
   static int grid = 0;  // resident blocks across the device (per instantiation)
   if (!grid) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_persistent<T, ST, M, W>, kBlock,
-                                                       (size_t)lds_cap(W) * kBlock * 8);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_persistent<T, ST, M, W, A>, kBlock,
+                                                       lds);
     grid = std::max(1, cus) * std::max(1, per_cu);
   }
   const uint64_t need = (F.n_items + kBlock - 1) / kBlock;
   const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);
-  hipLaunchKernelGGL((path_persistent<T, ST, M, W>), dim3(blocks), dim3(kBlock), (size_t)lds_cap(W) * kBlock * 8, st,
-                     S, F);
+  hipLaunchKernelGGL((path_persistent<T, ST, M, W, A>), dim3(blocks), dim3(kBlock), lds, st, S, F);
 }
-template <bool T, bool ST, int M>
+template <bool T, bool ST, int M, int A>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
-  switch (F.waves) {  // register budget: waves per SIMD the kernel is compiled for
-    case 7: launch_persistent_w<T, ST, M, 7>(S, F, st); break;
-    default: launch_persistent_w<T, ST, M, 6>(S, F, st); break;
-  }
+  if (A == ACC_BVH && F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);  // register budget (waves/SIMD)
+  else launch_persistent_w<T, ST, M, 6, A>(S, F, st);
 }
-template <bool T, bool ST>
+template <bool T, bool ST, int A>
 static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
   switch (F.mode) {
-    case MODE_AA: launch_persistent_m<T, ST, MODE_AA>(S, F, st); break;
-    case MODE_WHITTED_QUAD: launch_persistent_m<T, ST, MODE_WHITTED_QUAD>(S, F, st); break;
-    case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ>(S, F, st); break;
-    case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG>(S, F, st); break;
-    default: launch_persistent_m<T, ST, MODE_WHITTED_POINT>(S, F, st); break;
+    case MODE_AA: launch_persistent_m<T, ST, MODE_AA, A>(S, F, st); break;
+    case MODE_WHITTED_QUAD: launch_persistent_m<T, ST, MODE_WHITTED_QUAD, A>(S, F, st); break;
+    case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ, A>(S, F, st); break;
+    case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG, A>(S, F, st); break;
+    default: launch_persistent_m<T, ST, MODE_WHITTED_POINT, A>(S, F, st); break;
   }
 }
+template <int A>
+static void launch_persistent_a(const SceneArgs& S, const FrameArgs& F, bool tri_only, bool stats, hipStream_t st) {
+  if (tri_only) { if (stats) launch_persistent_t<true, true, A>(S, F, st); else launch_persistent_t<true, false, A>(S, F, st); }
+  else { if (stats) launch_persistent_t<false, true, A>(S, F, st); else launch_persistent_t<false, false, A>(S, F, st); }
+}
 
-bool persistent_supported(int accel, int mode) { return accel == ACC_BVH; }
+// BVH always; Grid when its cells pack into 10 bits per axis (the stepper's cell encoding)
+bool persistent_supported(int accel, const int gdim[3]) {
+  return accel == ACC_BVH || (accel == ACC_GRID && gdim[0] <= 1024 && gdim[1] <= 1024 && gdim[2] <= 1024);
+}
 
-void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, bool tri_only, bool stats, hipStream_t st) {
-  if (tri_only) { if (stats) launch_persistent_t<true, true>(S, F, st); else launch_persistent_t<true, false>(S, F, st); }
-  else { if (stats) launch_persistent_t<false, true>(S, F, st); else launch_persistent_t<false, false>(S, F, st); }
+void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats,
+                            hipStream_t st) {
+  if (accel == ACC_GRID) launch_persistent_a<ACC_GRID>(S, F, tri_only, stats, st);
+  else launch_persistent_a<ACC_BVH>(S, F, tri_only, stats, st);
 }
 
 void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats, hipStream_t st) {
