@@ -298,3 +298,19 @@ class Renderer:
         check(_lib.load().drt_trace_shadow(self.h, _fp(r), len(r), occ.ctypes.data_as(_lib._u8)), self.h,
               "drt_trace_shadow")
         return occ
+
+    def trace_device(self, shadow, d_rays, n, d_t=0, d_normal=0, d_object=0, d_occluded=0, stream=None):
+        """Asynchronous batched queries on device pointers (ints), on `stream` (int handle)."""
+        v = C.c_void_p
+        check(_lib.load().drt_trace_device(self.h, int(bool(shadow)), v(d_rays), int(n), v(d_t), v(d_normal),
+                                           v(d_object), v(d_occluded), v(stream or 0)), self.h, "drt_trace_device")
+
+    def set_trace_stats(self, on=True):
+        """Count traversal work (rays, nodes, leaves, primitives) of later batched queries."""
+        check(_lib.load().drt_set_trace_flags(self.h, FRAME_STATS if on else 0), self.h, "drt_set_trace_flags")
+
+    def trace_stats(self):
+        """Streaming-kernel time (kernel_ms) and counters of the last BVH batched query."""
+        s = DrtFrameStats()
+        check(_lib.load().drt_trace_stats(self.h, C.byref(s)), self.h, "drt_trace_stats")
+        return s.as_dict()

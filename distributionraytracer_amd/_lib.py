@@ -80,6 +80,9 @@ SIGNATURES = {
     "drt_unshard_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp, _vp]),
     "drt_trace_closest": (C.c_int, [_vp, _f, C.c_int32, _f, _f, _i32]),
     "drt_trace_shadow": (C.c_int, [_vp, _f, C.c_int32, _u8]),
+    "drt_trace_device": (C.c_int, [_vp, C.c_int, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp]),
+    "drt_set_trace_flags": (C.c_int, [_vp, C.c_int]),
+    "drt_trace_stats": (C.c_int, [_vp, C.POINTER(DrtFrameStats)]),
     "drt_get_stats": (C.c_int, [_vp, C.POINTER(DrtFrameStats)]),
     "drt_frame_times": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     # drt_host.h
@@ -144,7 +147,10 @@ def load():
             raise RuntimeError(f"{path} is missing: run distributionraytracer_amd._lib.build() "
                                "(make -C distributionraytracer_amd/csrc)")
         L = C.CDLL(str(path))
+        alt = bool(os.environ.get("DRT_LIBRARY"))
         for name, (res, args) in SIGNATURES.items():
+            if alt and not hasattr(L, name):
+                continue  # an older A/B build may predate an entry point the run does not call
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

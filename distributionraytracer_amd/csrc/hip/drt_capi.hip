@@ -20,6 +20,11 @@ void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, in
 bool persistent_supported(int accel, const int gdim[3]);
 void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats,
                             hipStream_t st);
+void launch_trace_stream(const SceneArgs& S, const TraceArgs& A, bool shadow, bool tri_only, bool stats, int waves,
+                         hipStream_t st);
+void launch_trace_prep(const float* rays, int n, int shadow, float4* out, hipStream_t st);
+void launch_trace_finish(const SceneArgs& S, const float4* q, int n, float* t, const uint32_t* prim, float* nrm,
+                         int32_t* obj, hipStream_t st);
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
                   float* nrm, int32_t* obj, uint8_t* occ, hipStream_t st);
 }  // namespace drt
@@ -87,6 +92,12 @@ struct drt_ctx {
   DevBuf d_samples, d_frame, d_stats, d_rays, d_out, d_counter;
   drt_frame_stats last{};
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
+  // batched queries: streaming-query records, primitive results, timing of the last call
+  DevBuf d_tq, d_tprim, d_tstats;
+  hipEvent_t tev[2] = {nullptr, nullptr};
+  int trace_flags = 0;        // DRT_FRAME_STATS: count traversal work of batched queries
+  bool trace_timed = false;   // the last batched query ran the streaming kernel
+  bool trace_stats_valid = false;
 };
 
 #define DRT_FAIL(ctx, code, ...)                                        \
@@ -156,6 +167,11 @@ int drt_create(drt_ctx** out, const drt_options* opt) {
       drt_destroy(c);
       return DRT_E_HIP;
     }
+  for (auto& e : c->tev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      drt_destroy(c);
+      return DRT_E_HIP;
+    }
   *out = c;
   return DRT_OK;
 }
@@ -165,6 +181,8 @@ void drt_destroy(drt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& e : c->ring)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->tev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -360,10 +378,10 @@ static int scene_args(drt_ctx* c, int accel, SceneArgs& S) {
   }
   if (accel == ACC_BVH) {
     if (!c->has_bvh) DRT_FAIL(c, DRT_E_STATE, "scene uses a BVH but none was uploaded");
+    S.big_leaves = c->d_big.as<uint2>();
     S.nodes = c->d_nodes.as<float4>();
     memcpy(S.root_box, c->root_box, sizeof(S.root_box));
     S.root_desc = c->root_desc;
-    S.big_leaves = c->d_big.as<uint2>();
   } else if (accel == ACC_GRID) {
     if (!c->has_grid) DRT_FAIL(c, DRT_E_STATE, "scene uses a grid but none was uploaded");
     memcpy(S.gdim, c->gdim, sizeof(S.gdim));
@@ -600,14 +618,56 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
   return DRT_OK;
 }
 
-static int trace_common(drt_ctx* c, const float* rays, int32_t n, int shadow, float* t, float* nrm, int32_t* obj,
-                        uint8_t* occ) {
-  if (!c || n < 0 || (n > 0 && !rays)) return DRT_E_INVALID;
-  if (n == 0) return DRT_OK;
+// Batched queries on device buffers, asynchronous on st.  BVH: prep -> streaming traversal
+// (timed with the context's trace events) -> closest-hit epilogue; Grid / NONE: trace_kernel.
+static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, float* dt, float* dn, int32_t* dobj,
+                        uint8_t* docc, hipStream_t st) {
   SceneArgs S;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
   int rc = scene_args(c, c->accel, S);
   if (rc) return rc;
+  DRT_HIP(c, hipSetDevice(c->device));
+  c->trace_timed = false;
+  c->trace_stats_valid = false;
+  if (c->accel != DRT_ACCEL_BVH) {
+    launch_trace(S, c->accel, c->tri_only, d_rays, n, shadow, dt, dn, dobj, docc, st);
+    DRT_HIP(c, hipGetLastError());
+    return DRT_OK;
+  }
+  DRT_HIP(c, c->d_tq.ensure(2 * sizeof(float4) * (size_t)n));
+  DRT_HIP(c, c->d_tprim.ensure(sizeof(uint32_t) * (size_t)n));
+  DRT_HIP(c, c->d_counter.ensure(256));
+  DRT_HIP(c, c->d_tstats.ensure(sizeof(unsigned long long) * ST_COUNT));
+  const bool stats = (c->trace_flags & DRT_FRAME_STATS) != 0;
+  float4* q = c->d_tq.as<float4>();
+  launch_trace_prep(d_rays, n, shadow, q, st);
+  DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 256, st));
+  if (stats) DRT_HIP(c, hipMemsetAsync(c->d_tstats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+  TraceArgs A{};
+  A.rays = q;
+  A.n = (uint32_t)n;
+  A.counter = c->d_counter.as<unsigned int>();
+  A.t_out = dt;
+  A.prim_out = c->d_tprim.as<uint32_t>();
+  A.occ_out = docc;
+  A.stats = c->d_tstats.as<unsigned long long>();
+  A.refill_min = env_int("DRT_TRACE_REFILL_MIN", 24);
+  DRT_HIP(c, hipEventRecord(c->tev[0], st));
+  launch_trace_stream(S, A, shadow != 0, c->tri_only, stats, env_int("DRT_TRACE_WAVES", 6), st);
+  DRT_HIP(c, hipGetLastError());
+  DRT_HIP(c, hipEventRecord(c->tev[1], st));
+  if (!shadow) launch_trace_finish(S, q, n, dt, A.prim_out, dn, dobj, st);
+  DRT_HIP(c, hipGetLastError());
+  c->trace_timed = true;
+  c->trace_stats_valid = stats;
+  return DRT_OK;
+}
+
+static int trace_common(drt_ctx* c, const float* rays, int32_t n, int shadow, float* t, float* nrm, int32_t* obj,
+                        uint8_t* occ) {
+  if (!c || n < 0 || (n > 0 && !rays)) return DRT_E_INVALID;
+  if (n == 0) return DRT_OK;
+  if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
   DRT_HIP(c, hipSetDevice(c->device));
   const size_t rb = sizeof(float) * 6 * (size_t)n;
   const size_t ob = shadow ? (size_t)n : (sizeof(float) * 4 + sizeof(int32_t)) * (size_t)n;
@@ -618,8 +678,8 @@ static int trace_common(drt_ctx* c, const float* rays, int32_t n, int shadow, fl
   float* dn = dt + n;
   int32_t* dobj = (int32_t*)(dn + 3 * (size_t)n);
   uint8_t* docc = c->d_out.as<uint8_t>();
-  launch_trace(S, c->accel, c->tri_only, c->d_rays.as<float>(), n, shadow, dt, dn, dobj, docc, c->stream);
-  DRT_HIP(c, hipGetLastError());
+  int rc = trace_device(c, c->d_rays.as<float>(), n, shadow, dt, dn, dobj, docc, c->stream);
+  if (rc) return rc;
   if (shadow) {
     DRT_HIP(c, hipMemcpyAsync(occ, docc, (size_t)n, hipMemcpyDeviceToHost, c->stream));
   } else {
@@ -628,6 +688,48 @@ static int trace_common(drt_ctx* c, const float* rays, int32_t n, int shadow, fl
     DRT_HIP(c, hipMemcpyAsync(obj, dobj, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
   }
   DRT_HIP(c, hipStreamSynchronize(c->stream));
+  return DRT_OK;
+}
+
+int drt_trace_device(drt_ctx* c, int shadow, const float* d_rays, int32_t n, float* d_t, float* d_normal,
+                     int32_t* d_object, uint8_t* d_occluded, void* hip_stream) {
+  if (!c || n < 0 || (n > 0 && !d_rays)) return DRT_E_INVALID;
+  if (shadow ? !d_occluded : (!d_t || !d_normal || !d_object)) return DRT_E_INVALID;
+  if (n == 0) return DRT_OK;
+  return trace_device(c, d_rays, n, shadow, d_t, d_normal, d_object, d_occluded,
+                      hip_stream ? (hipStream_t)hip_stream : c->stream);
+}
+
+int drt_set_trace_flags(drt_ctx* c, int flags) {
+  if (!c) return DRT_E_INVALID;
+  c->trace_flags = flags;
+  return DRT_OK;
+}
+
+int drt_trace_stats(drt_ctx* c, drt_frame_stats* out) {
+  if (!c || !out) return DRT_E_INVALID;
+  drt_frame_stats r{};
+  if (c->trace_timed) {
+    DRT_HIP(c, hipSetDevice(c->device));
+    DRT_HIP(c, hipEventSynchronize(c->tev[1]));
+    float ms = 0;
+    DRT_HIP(c, hipEventElapsedTime(&ms, c->tev[0], c->tev[1]));
+    r.kernel_ms = ms;
+    r.render_ms = ms;
+    if (c->trace_stats_valid) {
+      unsigned long long s[ST_COUNT];
+      DRT_HIP(c, hipMemcpy(s, c->d_tstats.p, sizeof(s), hipMemcpyDeviceToHost));
+      r.closest_rays = s[ST_CLOSEST]; r.shadow_rays = s[ST_SHADOW];
+      r.closest_inner = s[ST_C_INNER]; r.closest_leaf = s[ST_C_LEAF];
+      r.shadow_inner = s[ST_S_INNER]; r.shadow_leaf = s[ST_S_LEAF];
+      r.closest_prims = s[ST_C_PRIMS]; r.shadow_prims = s[ST_S_PRIMS];
+      r.wave_node_iters = s[ST_WAVE_NODE_ITERS];
+      r.stack_pushes = s[ST_PUSH];
+      r.stack_spills = s[ST_PUSH_SPILL];
+      r.wave_leaf_iters = s[ST_WAVE_LEAF_ITERS];
+    }
+  }
+  *out = r;
   return DRT_OK;
 }
 

@@ -890,12 +890,14 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // registers.  Without this a wave with lanes of both kinds paid two dependent round trips per
 // iteration.  Primitives past the second (SAH leaves, bvh.cpp:193) are fetched in pairs after.
 // (Measured alternative, kept out: one primitive per iteration — more iterations, 3 % slower.)
-template <bool TRI_ONLY, bool STATS, int CAP>
-__device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* lds, uint32_t* ov_desc,
+// KIND: 0 = the query kind is the lane's LF_SHADOW flag (path kernels), 1 = closest-hit only,
+// 2 = shadow only (the streaming traversal kernel's specialisations).
+template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, class LaneT>
+__device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kBlock * 4u;  // desc part; the t part follows
   uint32_t fl = L.fl;
-  const bool shadow = (fl & LF_SHADOW) != 0u;
+  const bool shadow = KIND == 0 ? (fl & LF_SHADOW) != 0u : KIND == 2;
   const uint32_t cur = L.cur;
   const bool visit = !(fl & LF_POP);
   const bool inner = visit && !desc_is_leaf(cur);
@@ -938,7 +940,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, Lane& L, LdsByte* 
     // are hit, and then tL, tR are non-NaN and >= 0 (or -0), so they order as sign-cleared
     // integers and `<=` is `< + 1`.
     const uint32_t uL = __float_as_uint(tL) & 0x7fffffffu, uR = __float_as_uint(tR) & 0x7fffffffu;
-    const bool left_first = uL < uR + (fl & LF_SHADOW);
+    const bool left_first = uL < uR + (KIND == 0 ? (fl & LF_SHADOW) : (KIND == 2 ? 1u : 0u));
     L.cur = (hL && (left_first || !hR)) ? d.x : d.y;
     fl |= (hL | hR) ? 0u : LF_POP;
     // push the far child (bvh.cpp:268-283); the LDS slot above the top is free, so the store
@@ -1383,6 +1385,140 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Streaming traversal: BVH::Traverse (bvh.cpp:231-314 closest, :316-391 shadow) over an array
+// of queries, one query per lane, lanes refilled from a global counter as they finish.  Only
+// the traversal state is live (ray, slab constants, node, stack pointer, best hit), so the
+// kernel runs at up to 8 waves per SIMD where the path kernel, which also carries shading
+// state, holds 6.  The node step is the path kernel's, specialised for one query kind.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kTraceChunk = 256;  // queries claimed per wave per atomic
+
+struct TLane {
+  uint32_t item, fl;
+  RayP q;
+  uint32_t cur, best_prim, spa;
+  float best_t, thr;
+};
+
+template <bool TRI_ONLY, int KIND, int WAVES, bool STATS>
+__global__ void __launch_bounds__(kBlock, WAVES) trace_stream(SceneArgs S, TraceArgs A) {
+  constexpr int CAP = lds_cap(WAVES);
+  static_assert(kBlock * 4 == 1024, "spa encoding assumes 256-thread blocks");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_bytes[];
+  uint32_t ov_desc[kMaxBvhDepth - CAP];
+  float ov_t[kMaxBvhDepth - CAP];
+  Counters C;
+  for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
+  uint64_t cyc_leaf = 0;
+  TLane L;
+  L.item = kNoItem;
+  L.fl = 0u;
+  L.spa = threadIdx.x * 4u;
+  const uint32_t lane = threadIdx.x & 63u;
+  // Queries are claimed kTraceChunk at a time per wave (one atomic), then handed to idle lanes
+  // from that wave-private range: one counter word serves only ~90 dequeues/us
+  // (MI355X_MICROARCH.md, dequeue), so a claim per refill would cap the kernel near 1 Gquery/s.
+  uint32_t chunk_next = 0, chunk_end = 0;  // wave-uniform
+  bool exhausted = false;                  // wave-uniform: the counter is past the end
+  while (true) {
+    const uint64_t idle = __ballot(L.item == kNoItem);
+    const int n_idle = __popcll(idle);
+    if (n_idle >= A.refill_min || n_idle == 64) {
+      if (chunk_next >= chunk_end && !exhausted) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(A.counter, kTraceChunk);
+        base = __shfl(base, 0, 64);
+        chunk_next = base;
+        chunk_end = base < A.n ? min(base + kTraceChunk, A.n) : base;
+        if (base + kTraceChunk >= A.n) exhausted = true;
+      }
+      if (L.item == kNoItem) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        const uint32_t it = chunk_next + rank;
+        if (it < chunk_end) {
+          const float4 a = A.rays[2 * (size_t)it], b = A.rays[2 * (size_t)it + 1];
+          L.item = it;
+          L.q = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
+          L.thr = a.w;
+          L.best_t = 3.402823466e+38f;
+          L.best_prim = 0xFFFFFFFFu;
+          L.spa &= 1023u;
+          L.cur = S.root_desc;
+          float tmp;
+          const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
+                                    S.root_box[5], L.q, tmp);  // bvh.cpp:242 / :328
+          L.fl = (KIND == 2 ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (ray_finite(L.q) ? LF_FINITE : 0u);
+          if (STATS) C.v[KIND == 2 ? ST_SHADOW : ST_CLOSEST]++;
+        }
+      }
+      chunk_next = min(chunk_next + (uint32_t)n_idle, chunk_end);
+    }
+    const bool in_trav = L.item != kNoItem && (L.fl & LF_TRAV);
+    const uint64_t trav = __ballot(in_trav);
+    if (trav) {
+      if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
+      const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
+      if (in_trav) node_step<TRI_ONLY, STATS, CAP, KIND>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc_leaf);
+    }
+    if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
+      if (KIND == 2) {
+        A.occ_out[L.item] = (L.fl & LF_HIT) ? 1 : 0;
+      } else {
+        const bool hit = (L.fl & LF_HIT) != 0u;
+        A.t_out[L.item] = hit ? L.best_t : 3.402823466e+38f;
+        A.prim_out[L.item] = hit ? L.best_prim : 0xFFFFFFFFu;
+      }
+      L.item = kNoItem;
+    } else if (!trav && exhausted && chunk_next >= chunk_end) {
+      break;
+    }
+  }
+  if (STATS) {
+    for (int s = 0; s < ST_COUNT; s++) {
+      unsigned long long v = C.v[s];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if (lane == 0 && v) atomicAdd(&A.stats[s], v);
+    }
+  }
+}
+
+// Batched-query front end: rays n x {ox,oy,oz,dx,dy,dz} -> streaming-query records with the
+// accelerator's range rule (BVH shadow: unit direction, |d| + EPSILON, bvh.cpp:321-322, :376).
+__global__ void __launch_bounds__(256) trace_prep_kernel(const float* __restrict__ rays, int n, int shadow,
+                                                         float4* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* rr = rays + 6 * (size_t)i;
+  V3 o = mk(rr[0], rr[1], rr[2]), d = mk(rr[3], rr[4], rr[5]);
+  float thr = 0.0f;
+  if (shadow) {
+    thr = shadow_threshold(length(d));
+    d = normalize(d);
+  }
+  out[2 * (size_t)i] = make_float4(o.x, o.y, o.z, thr);
+  out[2 * (size_t)i + 1] = make_float4(d.x, d.y, d.z, 0.0f);
+}
+
+// HitRecord normal and object index of each closest-hit result (the trace_kernel epilogue).
+__global__ void __launch_bounds__(256) trace_finish_kernel(SceneArgs S, const float4* __restrict__ q, int n,
+                                                           float* t_out, const uint32_t* __restrict__ prim,
+                                                           float* n_out, int32_t* obj_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = prim[i];
+  if (p == 0xFFFFFFFFu) {
+    n_out[3 * i] = 0.f; n_out[3 * i + 1] = 0.f; n_out[3 * i + 2] = 0.f;
+    obj_out[i] = -1;
+    return;
+  }
+  const float4 a = q[2 * (size_t)i], b = q[2 * (size_t)i + 1];
+  const RayP r = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
+  const V3 nn = prim_normal(S.prims, p, r, t_out[i]);
+  n_out[3 * i] = nn.x; n_out[3 * i + 1] = nn.y; n_out[3 * i + 2] = nn.z;
+  obj_out[i] = (int32_t)prim_object(S.prims[3 * p + 1]);
+}
+
 // Ordered sum over a pixel's items (Color += in sample order, main.cpp:664 / :694) and scale.
 __global__ void __launch_bounds__(256) reduce_kernel(ReduceArgs A) {
   const uint32_t pidx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1558,6 +1694,45 @@ void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, in
   const uint64_t n = (uint64_t)n_tiles * tile * tile;
   hipLaunchKernelGGL(unshard_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, shards, frame, tile, tiles_x,
                      n_tiles, n_shards, tiles_per_shard, res_x, res_y);
+}
+
+template <bool T, int K, int W, bool ST>
+static void launch_stream_w(const SceneArgs& S, const TraceArgs& A, hipStream_t st) {
+  const size_t lds = (size_t)lds_cap(W) * kBlock * 8;
+  static int grid = 0;  // resident blocks across the device (per instantiation)
+  if (!grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_stream<T, K, W, ST>, kBlock, lds);
+    grid = std::max(1, cus) * std::max(1, per_cu);
+  }
+  const uint64_t need = ((uint64_t)A.n + kBlock - 1) / kBlock;
+  const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)grid));
+  hipLaunchKernelGGL((trace_stream<T, K, W, ST>), dim3(blocks), dim3(kBlock), lds, st, S, A);
+}
+template <bool T, int K, bool ST>
+static void launch_stream_k(const SceneArgs& S, const TraceArgs& A, int waves, hipStream_t st) {
+  if (waves >= 8) launch_stream_w<T, K, 8, ST>(S, A, st);
+  else if (waves == 7) launch_stream_w<T, K, 7, ST>(S, A, st);
+  else launch_stream_w<T, K, 6, ST>(S, A, st);
+}
+void launch_trace_stream(const SceneArgs& S, const TraceArgs& A, bool shadow, bool tri_only, bool stats, int waves,
+                         hipStream_t st) {
+  if (tri_only) {
+    if (shadow) { if (stats) launch_stream_k<true, 2, true>(S, A, waves, st); else launch_stream_k<true, 2, false>(S, A, waves, st); }
+    else { if (stats) launch_stream_k<true, 1, true>(S, A, waves, st); else launch_stream_k<true, 1, false>(S, A, waves, st); }
+  } else {
+    if (shadow) { if (stats) launch_stream_k<false, 2, true>(S, A, waves, st); else launch_stream_k<false, 2, false>(S, A, waves, st); }
+    else { if (stats) launch_stream_k<false, 1, true>(S, A, waves, st); else launch_stream_k<false, 1, false>(S, A, waves, st); }
+  }
+}
+void launch_trace_prep(const float* rays, int n, int shadow, float4* out, hipStream_t st) {
+  hipLaunchKernelGGL(trace_prep_kernel, dim3((n + 255) / 256), dim3(256), 0, st, rays, n, shadow, out);
+}
+void launch_trace_finish(const SceneArgs& S, const float4* q, int n, float* t, const uint32_t* prim, float* nrm,
+                         int32_t* obj, hipStream_t st) {
+  hipLaunchKernelGGL(trace_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, st, S, q, n, t, prim, nrm, obj);
 }
 
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,

@@ -56,12 +56,12 @@ struct SceneArgs {
   const float4* nodes;
   float root_box[6];
   uint32_t root_desc;
-  const uint2* big_leaves;
   // Grid
   int gdim[3];
   float gmin[3], gmax[3];
   const uint32_t* cell_start;
   const uint32_t* cell_objs;
+  const uint2* big_leaves;
 };
 
 struct FrameArgs {
@@ -87,6 +87,18 @@ struct FrameArgs {
   int refill_min;              // persistent kernel: refill a wave once this many lanes are idle
   int process_min;             // persistent kernel: shade once this many lanes have a result
   int waves;                   // persistent kernel: register budget (waves per SIMD: 6 or 7)
+};
+
+// Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
+struct TraceArgs {
+  const float4* rays;          // 2 per query: (o.xyz, range threshold), (d.xyz, 0); shadow d is unit
+  uint32_t n;
+  unsigned int* counter;       // next unclaimed query (zeroed per launch)
+  float* t_out;                // closest: best t (FLT_MAX on a miss)
+  uint32_t* prim_out;          // closest: primitive record index (0xFFFFFFFF on a miss)
+  uint8_t* occ_out;            // shadow: 1 if occluded
+  unsigned long long* stats;   // ST_* counters (stats launches only)
+  int refill_min;
 };
 
 struct ReduceArgs {

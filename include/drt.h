@@ -187,6 +187,19 @@ int drt_unshard_device(drt_ctx* ctx, const drt_frame_params* params, const float
 int drt_trace_closest(drt_ctx* ctx, const float* rays, int32_t n, float* t, float* normal, int32_t* object);
 int drt_trace_shadow(drt_ctx* ctx, const float* rays, int32_t n, uint8_t* occluded);
 
+/* The same queries on DEVICE buffers, asynchronous on `hip_stream` (NULL = the context's
+ * stream): d_rays n x 6 floats; closest fills d_t / d_normal / d_object, shadow d_occluded.
+ * BVH scenes run the streaming traversal kernel (one query per lane, lanes refilled as they
+ * finish).  Replaces the same BVH/Grid Traverse calls as drt_trace_closest / drt_trace_shadow. */
+int drt_trace_device(drt_ctx* ctx, int shadow, const float* d_rays, int32_t n, float* d_t, float* d_normal,
+                     int32_t* d_object, uint8_t* d_occluded, void* hip_stream);
+/* flags for later batched queries: DRT_FRAME_STATS counts their traversal work */
+int drt_set_trace_flags(drt_ctx* ctx, int flags);
+/* Device time of the streaming traversal kernel of the most recent BVH batched query
+ * (kernel_ms) and, with DRT_FRAME_STATS set, its ray / node / leaf / primitive counters;
+ * zeroes for Grid / NONE queries.  Waits for that query. */
+int drt_trace_stats(drt_ctx* ctx, drt_frame_stats* out);
+
 /* Counters (frames rendered with DRT_FRAME_STATS) and device times of the most recent frame;
  * waits for that frame. */
 int drt_get_stats(drt_ctx* ctx, drt_frame_stats* out);

@@ -67,8 +67,12 @@ def synthetic_scene_text(n_tris, res=(512, 512), spp=64, accel="bvh", seed=1, ap
 
 
 def mixed_scene_text(res=(48, 40), spp=4, accel="bvh", seed=7, n_tris=300, aperture=0.0, focal=1.0, quad=True,
-                     glass=True, bclr=(0.078, 0.361, 0.753)):
-    """Spheres (mirror + glass), boxes, planes, triangles, quad + point lights."""
+                     glass=True, bclr=(0.078, 0.361, 0.753), cluster=0):
+    """Spheres (mirror + glass), boxes, planes, triangles, quad + point lights.
+
+    cluster > 0 adds `cluster` concentric spheres and `cluster` triangles spun about one
+    centroid: coincident centroids leave the SAH no split (bvh.cpp:187-189), so the BVH gets
+    oversized leaves (>= 31 objects, the layout's count-31 escape)."""
     rng = np.random.default_rng(seed)
     lines = header(res=res, spp=spp, accel=accel, aperture=aperture, focal=focal, bclr=bclr)
     if quad:
@@ -90,6 +94,18 @@ def mixed_scene_text(res=(48, 40), spp=4, accel="bvh", seed=7, n_tris=300, apert
     lines.append(f"box {vec((0.1, 0.1, -0.4))} {vec((0.5, 0.6, 0.0))}")
     lines.append("mat 0.6667 0.996 0.8745 0.75 1 1 1 0.25 100 0 1")
     t = synthetic_triangles(n_tris, seed) * 0.6
+    if cluster:
+        lines.append("mat 0.3 0.6 0.9 0.6 1 1 1 0.4 40 0 1")
+        for k in range(cluster):
+            lines.append(f"s {vec((-0.5, -0.5, 0.3))} {ff(0.05 + 0.004 * k)}")
+        a = np.linspace(0.0, np.pi, cluster, endpoint=False)[:, None]
+        c = np.array([0.55, -0.45, 0.35])
+        u = np.concatenate([np.cos(a), np.sin(a), 0 * a], 1) * 0.2
+        w = np.concatenate([-np.sin(a), np.cos(a), 0 * a], 1) * 0.1
+        # vertices c + u, c - u/2 + w*sqrt3, c - u/2 - w*sqrt3 ... centroid exactly c in exact math;
+        # float rounding may split a few, the rest stay together
+        spun = np.stack([c + u, c - u / 2 + w, c - u / 2 - w], 1).reshape(-1, 9)
+        t = np.concatenate([t, spun.astype(np.float32)])
     lines += mesh_lines(t)
     return "\n".join(lines) + "\n"
 

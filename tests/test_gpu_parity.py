@@ -127,7 +127,24 @@ RENDER_CASES = {
                                  {"roughness": 0.2}),
     "dof_glossy_depth8_bvh": (lambda: sg.mixed_scene_text(res=(24, 16), spp=9, accel="bvh", aperture=8.0,
                                                           focal=1.5), {"roughness": 0.1, "max_depth": 8}),
+    # oversized BVH leaves (>= 31 objects: count-31 descriptors, count in the first record)
+    "big_leaf_bvh": (lambda: sg.mixed_scene_text(res=(32, 24), spp=4, accel="bvh", cluster=40), {}),
+    "big_leaf_dof_bvh": (lambda: sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", cluster=40, aperture=8.0,
+                                                     focal=1.5), {}),
 }
+
+
+def test_big_leaf_traverse_matches_oracle(drt, oracle_mod, renderer, tmp_path):
+    a, b = load_both(drt, oracle_mod, tmp_path, sg.mixed_scene_text(accel="bvh", cluster=40))
+    renderer.upload(a)
+    rays = sg.random_rays(4000, seed=21)
+    rays[: len(rays) // 2, :3] = (-0.5, -0.5, 0.3)  # half start inside the concentric spheres
+    t, n, obj = renderer.trace_closest(rays)
+    rt, rn, ro = b.trace_closest(rays)
+    np.testing.assert_array_equal(obj, ro)
+    np.testing.assert_array_equal(bits(t), bits(rt))
+    np.testing.assert_array_equal(bits(n), bits(rn))
+    np.testing.assert_array_equal(renderer.trace_shadow(rays), b.trace_shadow(rays))
 
 
 @pytest.mark.parametrize("case", sorted(RENDER_CASES))
@@ -220,3 +237,51 @@ def test_full_size_frame_properties(drt, renderer, tmp_path):
     assert np.isfinite(a).all() and a.min() >= 0.0 and a.max() <= 1.0
     c = renderer.render(seed=4)
     assert (a != c).any()
+
+
+def test_trace_device_streaming_matches_reference_golden(drt, renderer, tmp_path):
+    """drt_trace_device (device buffers, streaming traversal kernel, several 256-query wave
+    chunks and a ragged tail) returns the reference's BVH::Traverse results bit for bit."""
+    import torch
+    from tests.test_oracle_pinning import GOLD
+
+    g = np.load(GOLD / "ref_tris2k.npz")
+    p = tmp_path / "s.p3f"
+    p.write_bytes(g["scene_text"].tobytes())
+    s = drt.Scene.load_p3f(p)
+    s.set_accel("bvh")
+    renderer.upload(s)
+    rays = torch.from_numpy(np.ascontiguousarray(g["rays"], np.float32)).cuda()
+    n = rays.shape[0]
+    t = torch.empty(n, dtype=torch.float32, device="cuda")
+    nrm = torch.empty((n, 3), dtype=torch.float32, device="cuda")
+    obj = torch.empty(n, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    renderer.set_trace_stats(True)
+    renderer.trace_device(False, rays.data_ptr(), n, t.data_ptr(), nrm.data_ptr(), obj.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    st = renderer.trace_stats()
+    renderer.set_trace_stats(False)
+    np.testing.assert_array_equal(obj.cpu().numpy(), g["bvh_obj"])
+    np.testing.assert_array_equal(bits(t.cpu().numpy()), bits(g["bvh_t"]))
+    np.testing.assert_array_equal(bits(nrm.cpu().numpy()), bits(g["bvh_n"]))
+    assert st["closest_rays"] == n and st["closest_inner"] > 0 and st["kernel_ms"] > 0
+    srays = torch.from_numpy(np.ascontiguousarray(g["shadow_rays"], np.float32)).cuda()
+    occ = torch.empty(srays.shape[0], dtype=torch.uint8, device="cuda")
+    renderer.trace_device(True, srays.data_ptr(), srays.shape[0], d_occluded=occ.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(occ.cpu().numpy(), g["bvh_occ"])
+
+
+def test_streaming_traverse_many_chunks_matches_oracle(drt, oracle_mod, renderer, tmp_path):
+    """60k queries (hundreds of wave chunks) on a 20k-triangle soup: closest and shadow results
+    equal the oracle's BVH::Traverse restatement."""
+    a, b = load_both(drt, oracle_mod, tmp_path, sg.synthetic_scene_text(20000, res=(8, 8), spp=1))
+    renderer.upload(a)
+    rays = sg.random_rays(60001, seed=33, origin_box=2.0)
+    t, n, obj = renderer.trace_closest(rays)
+    rt, rn, ro = b.trace_closest(rays)
+    np.testing.assert_array_equal(obj, ro)
+    np.testing.assert_array_equal(bits(t), bits(rt))
+    np.testing.assert_array_equal(bits(n), bits(rn))
+    np.testing.assert_array_equal(renderer.trace_shadow(rays), b.trace_shadow(rays))

@@ -110,6 +110,18 @@ def test_parallel_bvh_build_matches_oracle_large(oracle_mod, tmp_path):
     np.testing.assert_array_equal(bits(x["boxes"]), bits(y["boxes"]))
 
 
+def test_cluster_scene_has_oversized_leaf_matching_oracle(oracle_mod, tmp_path):
+    """The `cluster` scene of the GPU big-leaf cases really yields a leaf of >= 31 objects
+    (the count-31 descriptor path), in the same tree as the oracle's build."""
+    a, b = _both(oracle_mod, tmp_path, sg.mixed_scene_text(accel="bvh", cluster=40))
+    a.build()
+    b.build()
+    x, y = a.bvh_export(), b.bvh_export()
+    for k in ("leaf", "index", "nobjs", "order"):
+        np.testing.assert_array_equal(x[k], y[k], err_msg=k)
+    assert (np.asarray(x["nobjs"])[np.asarray(x["leaf"]).astype(bool)] >= 31).any()
+
+
 def test_camera_frame_matches_reference_golden():
     g = np.load(GOLD / "ref_misc.npz")
     for ci, c in enumerate(g["cam_params"]):
