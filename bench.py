@@ -59,14 +59,33 @@ def populate(scene, tris, res, spp, aperture=0.0, focal=1.0, accel="bvh", ks=0.5
     scene.add_triangles(tris)
 
 
-def cpu_baseline(tris, res, spp, seed, target_s, threads, ext):
+def balls_low_path(res, spp, accel):
+    """BASELINE config C2: P3D_Scenes/balls_low (spheres + plane, 2 quad + 1 point light) as P3F
+    text with resolution / spp / accel set (tests/scenegen.py restates the scene file)."""
+    import tempfile
+
+    from tests import scenegen
+
+    d = Path(tempfile.mkdtemp(prefix="drt_bench_"))
+    return scenegen.write(d, "balls_low.p3f", scenegen.balls_low_text(res=(res, res), spp=spp, accel=accel))
+
+
+def make_scene(mod, args, tris, ext):
+    """The bench scene for the product (mod = distributionraytracer_amd) or the oracle."""
+    if args.scene == "balls_low":
+        return mod.Scene.load_p3f(balls_low_path(args.res, args.spp, ext["accel"]))
+    s = mod.Scene.new() if hasattr(mod.Scene, "new") else mod.Scene()
+    populate(s, tris, args.res, args.spp, ext["aperture"], ext["focal"], ext["accel"], ext["ks"])
+    return s
+
+
+def cpu_baseline(args, tris, res, spp, seed, target_s, threads, ext):
     """The CPU oracle (C++/OpenMP restatement of the reference, oracle/) timed on this host on a
     bounded sample: a band of full rows of the SAME frame."""
     from oracle import oracle as O
 
     O.build()
-    s = O.Scene.new()
-    populate(s, tris, res, spp, ext["aperture"], ext["focal"], ext["accel"], ext["ks"])
+    s = make_scene(O, args, tris, ext)
     kw = {k: ext[k] for k in ("max_depth", "roughness", "light_spp")}
     t0 = time.time()
     s.build()
@@ -92,6 +111,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="synthetic", choices=["synthetic", "balls_low"],
+                    help="synthetic triangle soup (headline, C3, C4) or P3D_Scenes balls_low (C2)")
     ap.add_argument("--tris", type=int, default=1_000_000)
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--spp", type=int, default=64)
@@ -140,11 +161,10 @@ def main():
             print(*a, file=sys.stderr, flush=True)
 
     t0 = time.time()
-    tris = synthetic_triangles(args.tris, args.seed)
-    scene = drt.Scene()
+    tris = synthetic_triangles(args.tris, args.seed) if args.scene == "synthetic" else None
     ext = {"aperture": args.aperture, "focal": args.focal, "roughness": args.roughness,
            "max_depth": args.max_depth, "light_spp": args.light_spp, "accel": args.accel, "ks": args.ks}
-    populate(scene, tris, args.res, args.spp, args.aperture, args.focal, args.accel, args.ks)
+    scene = make_scene(drt, args, tris, ext)
     scene.build()
     info = scene.info()
     build_s = time.time() - t0
@@ -235,7 +255,8 @@ def main():
     traffic = None
     dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh", "ks": 0.5}
     extras = [f"{k}{v if isinstance(v, str) else format(v, 'g')}" for k, v in ext.items() if v != dflt[k]]
-    workload_key = "_".join([f"tris{args.tris}_res{args.res}_spp{args.spp}"] + extras)
+    head = f"tris{args.tris}" if args.scene == "synthetic" else args.scene
+    workload_key = "_".join([f"{head}_res{args.res}_spp{args.spp}"] + extras)
     tj = Path(args.traffic_json)
     if world == 1 and tj.exists():
         try:
@@ -258,17 +279,20 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded random triangle soup, SURVEY.md §8d)",
-        "config": {"workload": f"synthetic {args.tris} triangles + floor, {args.accel.upper()}, {args.res}x{args.res}, "
-                               f"{args.spp} spp, MAX_DEPTH {args.max_depth}, 1 quad + 1 point light"
+        "data": ("synthetic (seeded random triangle soup, SURVEY.md §8d)" if args.scene == "synthetic" else
+                 "balls_low scene (reference P3F content, tests/scenegen.py)"),
+        "config": {"workload": (f"synthetic {args.tris} triangles + floor" if args.scene == "synthetic" else
+                                "P3D_Scenes balls_low (10 spheres + plane)")
+                               + f", {args.accel.upper()}, {args.res}x{args.res}, {args.spp} spp, MAX_DEPTH {args.max_depth}, "
+                               + ("1 quad + 1 point light" if args.scene == "synthetic" else "2 quad + 1 point light")
                                + (f", DoF aperture {args.aperture:g} focal {args.focal:g}" if args.aperture else "")
                                + (f", roughness {args.roughness:g}" if args.roughness else "")
                                + (f", {args.light_spp} quad-light samples" if args.light_spp > 1 else ""),
-                   "tris": args.tris, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
+                   "scene": args.scene, "tris": args.tris if args.scene == "synthetic" else 0, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
                    "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "path_kernel<BVH,tri>", "bytes_per_launch": int(bytes_launch),
+                     "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3)},
         "host_output_frame_ms": None if host_frame_ms is None else round(host_frame_ms, 3),
         **({"frame_check_vs_whole_frame": frame_check} if args.check_frame else {}),
@@ -303,7 +327,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(tris, args.res, args.spp, args.seed, args.cpu_seconds, threads, ext)
+            out["cpu_baseline"] = cpu_baseline(args, tris, args.res, args.spp, args.seed, args.cpu_seconds, threads,
+                                               ext)
             out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         except Exception as e:  # the baseline is reported, never required
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
