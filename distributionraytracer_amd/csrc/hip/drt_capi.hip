@@ -495,9 +495,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   DRT_HIP(c, hipEventRecord(ev[0], st));
   const bool persistent = P.persistent;
   if (persistent) {
-    DRT_HIP(c, c->d_counter.ensure(256));
-    DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 256, st));
+    DRT_HIP(c, c->d_counter.ensure(1024));
+    DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 1024, st));  // 8 partition counters, 64 B apart
     P.F.work_counter = c->d_counter.as<unsigned int>();
+    P.F.part_items = (uint32_t)((P.F.n_items + 7) / 8);
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
     P.F.process_min = env_int("DRT_PROCESS_MIN", 24);
     P.F.waves = env_int("DRT_WAVES", 6);
@@ -636,7 +637,7 @@ static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, 
   }
   DRT_HIP(c, c->d_tq.ensure(2 * sizeof(float4) * (size_t)n));
   DRT_HIP(c, c->d_tprim.ensure(sizeof(uint32_t) * (size_t)n));
-  DRT_HIP(c, c->d_counter.ensure(256));
+  DRT_HIP(c, c->d_counter.ensure(1024));
   DRT_HIP(c, c->d_tstats.ensure(sizeof(unsigned long long) * ST_COUNT));
   const bool stats = (c->trace_flags & DRT_FRAME_STATS) != 0;
   float4* q = c->d_tq.as<float4>();

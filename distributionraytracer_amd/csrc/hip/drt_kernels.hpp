@@ -87,6 +87,7 @@ struct FrameArgs {
   int refill_min;              // persistent kernel: refill a wave once this many lanes are idle
   int process_min;             // persistent kernel: shade once this many lanes have a result
   int waves;                   // persistent kernel: register budget (waves per SIMD: 6 or 7)
+  uint32_t part_items;         // persistent kernel: items per XCD work partition (ceil(n_items / 8))
 };
 
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
