@@ -1371,7 +1371,12 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
     const uint64_t t2 = stamp();
     // ---- batched shading for lanes whose query completed
     const bool done = live && !(L.fl & LF_TRAV);
-    if (ready && (__popcll(ready) >= F.process_min || trav == 0 || exhausted)) {
+    // Once every item is claimed, AA-style frames shade any ready lane (the frame is ending);
+    // in-order (MODE_SEQ) frames reach that point with each lane still holding a pixel's
+    // remaining samples, so they keep batching until half the live lanes are ready (C4:
+    // shading SIMD efficiency 0.10 -> 0.33, +2.7 %; on MODE_AA the same rule costs 1.4 %).
+    const bool drain = MODE == MODE_SEQ ? (exhausted && 2 * __popcll(ready) >= __popcll(ready | trav)) : exhausted;
+    if (ready && (__popcll(ready) >= F.process_min || trav == 0 || drain)) {
       if (STATS) {
         if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
         if (done) C.v[ST_LANE_PATH_ITERS]++;
