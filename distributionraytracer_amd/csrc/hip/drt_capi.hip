@@ -87,7 +87,8 @@ struct drt_ctx {
   bool has_grid = false;
   int gdim[3] = {0, 0, 0};
   float gmin[3] = {0}, gmax[3] = {0};
-  DevBuf d_cell_start, d_cell_objs;
+  DevBuf d_cell_start, d_cell_objs, d_macro, d_cell_recs;
+  int gmacro_shift = 0, gmacro_dim[3] = {0, 0, 0}, gmacro_words = 0;
   // frame scratch
   DevBuf d_samples, d_frame, d_stats, d_rays, d_out, d_counter;
   drt_frame_stats last{};
@@ -345,9 +346,41 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   DRT_HIP(c, hipMemcpy(c->d_cell_start.p, s32.data(), 4 * s32.size(), hipMemcpyHostToDevice));
   DRT_HIP(c, c->d_cell_objs.ensure(4 * std::max<size_t>(1, o32.size())));
   if (!o32.empty()) DRT_HIP(c, hipMemcpy(c->d_cell_objs.p, o32.data(), 4 * o32.size(), hipMemcpyHostToDevice));
+  // the persistent Grid stepper reads the referenced records inline, in cell order (48 B per
+  // reference; q2.w = the scene-order primitive index), so a cell's objects are one hop away
+  {
+    std::vector<PrimRecord> recs((size_t)std::max<int64_t>(1, n_refs));
+    for (int64_t i = 0; i < n_refs; i++) {
+      recs[i] = c->prims_scene[o32[i]];
+      memcpy(&recs[i].q[11], &o32[i], 4);
+    }
+    DRT_HIP(c, c->d_cell_recs.ensure(sizeof(PrimRecord) * recs.size() + kPrimPadBytes));
+    DRT_HIP(c, hipMemset(c->d_cell_recs.p, 0, sizeof(PrimRecord) * recs.size() + kPrimPadBytes));
+    DRT_HIP(c, hipMemcpy(c->d_cell_recs.p, recs.data(), sizeof(PrimRecord) * recs.size(), hipMemcpyHostToDevice));
+  }
   // grid references index scene-order primitive records
   DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
                        hipMemcpyHostToDevice));
+  // macro-cell occupancy bitmap (2^ms cells per side, <= kMacroBits bits): the Grid stepper keeps it
+  // in LDS and steps through empty macro-cells without touching memory
+  int ms = 0;
+  auto mdim = [&](int d, int m) { return (d + (1 << m) - 1) >> m; };
+  while ((size_t)mdim(dims[0], ms) * mdim(dims[1], ms) * mdim(dims[2], ms) > kMacroBits) ms++;
+  const int mx = mdim(dims[0], ms), my = mdim(dims[1], ms), mz = mdim(dims[2], ms);
+  std::vector<uint32_t> bits(((size_t)mx * my * mz + 31) / 32, 0u);
+  for (int z = 0; z < dims[2]; z++)
+    for (int y = 0; y < dims[1]; y++)
+      for (int x = 0; x < dims[0]; x++) {
+        const size_t ci = (size_t)x + (size_t)dims[0] * y + (size_t)dims[0] * dims[1] * z;
+        if (s32[ci + 1] == s32[ci]) continue;
+        const size_t mi = (size_t)(x >> ms) + (size_t)mx * (y >> ms) + (size_t)mx * my * (z >> ms);
+        bits[mi >> 5] |= 1u << (mi & 31);
+      }
+  DRT_HIP(c, c->d_macro.ensure(4 * bits.size()));
+  DRT_HIP(c, hipMemcpy(c->d_macro.p, bits.data(), 4 * bits.size(), hipMemcpyHostToDevice));
+  c->gmacro_shift = ms;
+  c->gmacro_dim[0] = mx; c->gmacro_dim[1] = my; c->gmacro_dim[2] = mz;
+  c->gmacro_words = (int)bits.size();
   memcpy(c->gdim, dims, sizeof(c->gdim));
   memcpy(c->gmin, bmin, sizeof(c->gmin));
   memcpy(c->gmax, bmax, sizeof(c->gmax));
@@ -388,6 +421,11 @@ static int scene_args(drt_ctx* c, int accel, SceneArgs& S) {
     memcpy(S.gmin, c->gmin, sizeof(S.gmin));
     memcpy(S.gmax, c->gmax, sizeof(S.gmax));
     S.cell_start = c->d_cell_start.as<uint32_t>();
+    S.gmacro = c->d_macro.as<uint32_t>();
+    S.cell_recs = c->d_cell_recs.as<float4>();
+    S.gmacro_shift = c->gmacro_shift;
+    memcpy(S.gmacro_dim, c->gmacro_dim, sizeof(S.gmacro_dim));
+    S.gmacro_words = c->gmacro_words;
     S.cell_objs = c->d_cell_objs.as<uint32_t>();
   }
   return DRT_OK;

@@ -35,6 +35,7 @@ constexpr int kMaxFrames = 16;     // max_depth <= 15
 constexpr int kMaxBvhDepth = 96;   // traversal stack entries (host rejects deeper trees)
 constexpr int kLdsStack = 16;      // traversal stack entries kept in LDS per thread
 constexpr int kBlock = 256;        // path-kernel block size
+constexpr size_t kMacroBits = 131072;  // Grid macro-cell bitmap budget: 16 KB of LDS per block
 constexpr size_t kPrimPadBytes = 64;  // zeroed tail of the primitive buffer (node_step's slot reads)
 
 struct SceneArgs {
@@ -61,6 +62,11 @@ struct SceneArgs {
   float gmin[3], gmax[3];
   const uint32_t* cell_start;
   const uint32_t* cell_objs;
+  // macro-cell occupancy bitmap: bit (x>>shift) + mx*((y>>shift) + my*(z>>shift)) set if any
+  // cell of that macro-cell holds an object
+  const uint32_t* gmacro;
+  const float4* cell_recs;  // per reference, in cell order: the primitive record, q2.w = its index
+  int gmacro_shift, gmacro_dim[3], gmacro_words;
   const uint2* big_leaves;
 };
 
