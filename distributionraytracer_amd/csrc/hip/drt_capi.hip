@@ -329,6 +329,15 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
                     const int32_t* co, int64_t n_refs) {
   if (!c || !dims || !bmin || !bmax || !cs || (n_refs > 0 && !co)) return DRT_E_INVALID;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its grid");
+  // A scene without objects: Grid::Build's widths overflow (float FLT_MAX - -FLT_MAX), the cell
+  // counts come out NaN -> INT_MIN and the grid has no cells (grid.cpp:56-67); its box is
+  // inverted, so every ray misses it.  Same here with one empty cell under that box.
+  static const int64_t kEmptyStart[2] = {0, 0};
+  static const int32_t kOneCell[3] = {1, 1, 1};
+  if (n_refs == 0 && (dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0)) {
+    dims = kOneCell;
+    cs = kEmptyStart;
+  }
   if (dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0) DRT_FAIL(c, DRT_E_INVALID, "bad grid dims");
   if (n_refs >= (int64_t)0xFFFFFFFF) DRT_FAIL(c, DRT_E_UNSUPPORTED, "too many grid references");
   const size_t ncell = (size_t)dims[0] * dims[1] * dims[2];

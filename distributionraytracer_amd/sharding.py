@@ -2,10 +2,12 @@
 
 Pixels are independent (main.cpp:603: the reference parallelises the pixel loop) and the keyed
 RNG depends only on (seed, pixel, call index), so a frame splits into square tiles dealt
-round-robin: tile t (row-major over ceil(RES_X/tile) x ceil(RES_Y/tile) tiles) belongs to rank
-t % n_shards.  Each rank renders its tiles into a shard-compact buffer (drt_render_device with
-n_shards > 1): its k-th tile (t = shard + k * n_shards) occupies floats
-[k * tile^2 * 3, (k + 1) * tile^2 * 3), pixel (px, py) of the tile at (py * tile + px) * 3.
+round-robin over a dealing order in which tile row ty is rotated by ty tiles: tile (tx, ty) has
+position p = ty * tiles_x + (tx + ty) % tiles_x and belongs to rank p % n_shards, so every rank
+takes diagonal stripes of the image rather than the same columns in every row.  Each rank
+renders its tiles into a shard-compact buffer (drt_render_device with n_shards > 1): its k-th
+tile (position p = shard + k * n_shards) occupies floats [k * tile^2 * 3, (k + 1) * tile^2 * 3),
+pixel (px, py) of the tile at (py * tile + px) * 3.
 Every shard buffer has the same length (tiles_per_shard = ceil(n_tiles / n_shards) tiles), so
 the gather is one all_gather_into_tensor (RCCL over xGMI on GPUs, gloo on CPU) and the frame is
 reassembled by drt_unshard_device.  The numpy pack/unshard mirrors below define that layout for
@@ -49,9 +51,18 @@ class TileLayout:
     def floats_per_shard(self) -> int:
         return self.tiles_per_shard * self.tile * self.tile * 3
 
-    def tiles_of(self, shard: int) -> range:
-        """Tile indices rendered by `shard` (drt_frame_params.shard)."""
-        return range(shard, self.n_tiles, self.n_shards)
+    def position_of_tile(self, t: int) -> int:
+        """Dealing position of row-major tile t (tile_of_position in drt_kernels.hip)."""
+        tx, ty = t % self.tiles_x, t // self.tiles_x
+        return ty * self.tiles_x + (tx + ty) % self.tiles_x
+
+    def tile_of_position(self, p: int) -> int:
+        ty, r = divmod(p, self.tiles_x)
+        return ty * self.tiles_x + (r - ty) % self.tiles_x
+
+    def tiles_of(self, shard: int) -> list[int]:
+        """Row-major tile indices rendered by `shard` (drt_frame_params.shard), in buffer order."""
+        return [self.tile_of_position(p) for p in range(shard, self.n_tiles, self.n_shards)]
 
     def tile_origin(self, t: int) -> tuple[int, int]:
         return (t % self.tiles_x) * self.tile, (t // self.tiles_x) * self.tile
@@ -75,7 +86,8 @@ class TileLayout:
             x0, y0 = self.tile_origin(t)
             h = min(self.tile, self.res_y - y0)
             w = min(self.tile, self.res_x - x0)
-            frame[y0:y0 + h, x0:x0 + w] = g[t % self.n_shards, t // self.n_shards, :h, :w]
+            p = self.position_of_tile(t)
+            frame[y0:y0 + h, x0:x0 + w] = g[p % self.n_shards, p // self.n_shards, :h, :w]
         return frame
 
 

@@ -67,14 +67,14 @@ def synthetic_scene_text(n_tris, res=(512, 512), spp=64, accel="bvh", seed=1, ap
 
 
 def mixed_scene_text(res=(48, 40), spp=4, accel="bvh", seed=7, n_tris=300, aperture=0.0, focal=1.0, quad=True,
-                     glass=True, bclr=(0.078, 0.361, 0.753), cluster=0):
+                     glass=True, bclr=(0.078, 0.361, 0.753), cluster=0, env=None):
     """Spheres (mirror + glass), boxes, planes, triangles, quad + point lights.
 
     cluster > 0 adds `cluster` concentric spheres and `cluster` triangles spun about one
     centroid: coincident centroids leave the SAH no split (bvh.cpp:187-189), so the BVH gets
     oversized leaves (>= 31 objects, the layout's count-31 escape)."""
     rng = np.random.default_rng(seed)
-    lines = header(res=res, spp=spp, accel=accel, aperture=aperture, focal=focal, bclr=bclr)
+    lines = header(res=res, spp=spp, accel=accel, aperture=aperture, focal=focal, bclr=bclr, env=env)
     if quad:
         lines.append("light quad 4 3 2 1 1 1 4 2 2 3 3 2 4")
     lines.append("light punctual -3 1 5 1 1 1")

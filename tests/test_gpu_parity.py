@@ -285,3 +285,87 @@ def test_streaming_traverse_many_chunks_matches_oracle(drt, oracle_mod, renderer
     np.testing.assert_array_equal(bits(t), bits(rt))
     np.testing.assert_array_equal(bits(n), bits(rn))
     np.testing.assert_array_equal(renderer.trace_shadow(rays), b.trace_shadow(rays))
+
+
+# BASELINE.json configs at their full sizes: the GPU renders the whole frame, the oracle a band
+# of rows of the same frame (its cost is per row; the keyed RNG makes rows independent).
+FULL_SIZE = {
+    # name: (scene, render kwargs, oracle rows (None = the whole frame))
+    "C2_balls_low_bvh_512_16spp": (dict(scene="balls_low", res=512, spp=16), {}, None),
+    "C3_tri100k_512_64spp_soft4": (dict(tris=100_000, res=512, spp=64), {"light_spp": 4}, (300, 304)),
+    "headline_tri1M_512_64spp": (dict(tris=1_000_000, res=512, spp=64), {}, (250, 254)),
+    "C4_tri1M_1024_64spp_dof_glossy_depth8": (dict(tris=1_000_000, res=1024, spp=64, aperture=8.0, focal=1.0),
+                                              {"roughness": 0.1, "max_depth": 8}, (600, 602)),
+}
+
+
+@pytest.mark.parametrize("case", sorted(FULL_SIZE))
+def test_full_size_config_matches_oracle(drt, oracle_mod, renderer, case):
+    import types
+
+    import bench
+
+    sk, kw, rows = FULL_SIZE[case]
+    args = types.SimpleNamespace(scene=sk.get("scene", "synthetic"), res=sk["res"], spp=sk["spp"])
+    ext = {"aperture": sk.get("aperture", 0.0), "focal": sk.get("focal", 1.0), "accel": "bvh", "ks": 0.5}
+    tris = bench.synthetic_triangles(sk["tris"], 1) if "tris" in sk else None
+    a = bench.make_scene(drt, args, tris, ext)
+    a.build()
+    renderer.upload(a)
+    img = renderer.render(seed=7, **kw)
+    b = bench.make_scene(oracle_mod, args, tris, ext)
+    b.build()
+    ref, _ = b.render(seed=7, rows=rows, **kw)
+    y0, y1 = rows if rows else (0, sk["res"])
+    compare_images(img[y0:y1], ref[y0:y1])
+    if rows:  # rows outside the band: rendered, finite, clamped
+        assert np.isfinite(img).all() and img.min() >= 0.0 and img.max() <= 1.0
+
+
+@pytest.mark.parametrize("accel,spp", [("bvh", 4), ("grid", 0), ("none", 4)])
+def test_skybox_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, accel, spp):
+    """Misses and mirror bounces that leave the scene read the cube map (scene.cpp:380-458):
+    six random bottom-up RGB8 faces of different sizes fed to both sides."""
+    rng = np.random.default_rng(17)
+    faces = [rng.integers(0, 256, size=(12 + 4 * i, 12 + 4 * i, 3), dtype=np.uint8) for i in range(6)]
+    text = sg.mixed_scene_text(res=(40, 32), spp=spp, accel=accel, n_tris=60, env="sky")
+    p = sg.write(tmp_path, "sky.p3f", text)
+    a = drt.Scene.load_p3f(p, skybox_faces=faces)
+    b = oracle_mod.Scene.load_p3f(p, skybox_faces=faces)
+    renderer.upload(a)
+    img = renderer.render(seed=5)
+    ref, _ = b.render(seed=5)
+    compare_images(img, ref)
+    bg = np.array([0.078, 0.361, 0.753], np.float32)
+    assert (np.abs(img - bg).max(axis=-1) > 1e-3).mean() > 0.9  # the sky, not bclr, fills the misses
+
+
+EDGE_CASES = {
+    # no objects: every ray misses (root / grid box inverted, NONE scans nothing)
+    "empty_bvh": lambda: "\n".join(sg.header(res=(24, 16), spp=4, accel="bvh") + ["light punctual -3 1 5 1 1 1"]) + "\n",
+    "empty_grid": lambda: "\n".join(sg.header(res=(24, 16), spp=0, accel="grid") + ["light punctual -3 1 5 1 1 1"]) + "\n",
+    "empty_none": lambda: "\n".join(sg.header(res=(24, 16), spp=4, accel="none")) + "\n",
+}
+
+
+@pytest.mark.parametrize("case", sorted(EDGE_CASES))
+def test_edge_scene_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
+    a, b = load_both(drt, oracle_mod, tmp_path, EDGE_CASES[case]())
+    renderer.upload(a)
+    img = renderer.render(seed=3)
+    ref, _ = b.render(seed=3)
+    compare_images(img, ref)
+    np.testing.assert_allclose(img, np.broadcast_to(np.float32([0.078, 0.361, 0.753]), img.shape), atol=1e-6)
+
+
+def test_no_lights_and_deepest_recursion_match_oracle(drt, oracle_mod, renderer, tmp_path):
+    """No lights: secondary rays get lightPos (0,0,0) (Q2) and only reflections/refractions add
+    colour; MAX_DEPTH 15 is the deepest call chain the frame stack holds (kMaxFrames - 1)."""
+    lines = sg.mixed_scene_text(res=(32, 24), spp=4, accel="bvh", n_tris=80).split("\n")
+    text = "\n".join(l for l in lines if not l.startswith("light")) + "\n"
+    a, b = load_both(drt, oracle_mod, tmp_path, text)
+    renderer.upload(a)
+    for kw in ({}, {"max_depth": 15}):
+        img = renderer.render(seed=8, **kw)
+        ref, _ = b.render(seed=8, **kw)
+        compare_images(img, ref)
