@@ -127,6 +127,9 @@ def main():
     ap.add_argument("--ks", type=float, default=0.5, help="material Ks (0: no mirror bounces; diagnostics)")
     ap.add_argument("--check-frame", action="store_true",
                     help="after timing, rank 0 checks the assembled frame against a whole-frame render (bitwise)")
+    ap.add_argument("--frames-in-flight", type=int, default=2, choices=[1, 2],
+                    help="frames pipelined on separate streams and scratch slots (2: a frame's start overlaps "
+                         "the previous frame's tail)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
@@ -176,25 +179,33 @@ def main():
     sptr = stream.cuda_stream
 
     fkw = {"max_depth": args.max_depth, "roughness": args.roughness, "light_spp": args.light_spp}
-    shard_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, **fkw)
+    pipe = args.frames_in_flight
+    shard_ps = [r.frame_params(seed=args.seed, shard=rank, n_shards=world, slot=j, **fkw) for j in range(pipe)]
+    shard_p = shard_ps[0]
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
     frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
+    # frames in flight: frame i runs on stream / scratch slot / output buffers i % pipe, so the next
+    # frame's kernel fills the CUs the previous frame's tail leaves idle
+    streams = [stream] + [torch.cuda.Stream() for _ in range(pipe - 1)]
+    frames = [frame] + [torch.empty_like(frame) for _ in range(pipe - 1)]
     if world > 1:
         layout = TileLayout(args.res, args.res, 16, world)
         tiles, floats = r.shard_layout(shard_p)
         if floats != layout.floats_per_shard or tiles != len(layout.tiles_of(rank)):
             raise RuntimeError(f"shard layout mismatch: library {tiles} tiles / {floats} floats, "
                                f"host {len(layout.tiles_of(rank))} / {layout.floats_per_shard}")
-        fg = FrameGather(layout, device="cuda")
+        fgs = [FrameGather(layout, device="cuda") for _ in range(pipe)]
 
-    def step(p):
-        if world == 1:
-            r.render_device(p, frame.data_ptr(), sptr)
-        else:
-            r.render_device(p, fg.shard.data_ptr(), sptr)
-            gathered = fg.gather()  # RCCL all-gather of the shard buffers over xGMI
-            if rank == 0:
-                r.unshard_device(shard_p, gathered.data_ptr(), frame.data_ptr(), sptr)
+    def step(p, j=0):
+        s = streams[j]
+        with torch.cuda.stream(s):
+            if world == 1:
+                r.render_device(p, frames[j].data_ptr(), s.cuda_stream)
+            else:
+                r.render_device(p, fgs[j].shard.data_ptr(), s.cuda_stream)
+                gathered = fgs[j].gather()  # RCCL all-gather of the shard buffers over xGMI
+                if rank == 0:
+                    r.unshard_device(p, gathered.data_ptr(), frames[j].data_ptr(), s.cuda_stream)
 
     # untimed stats frame: rays, node visits and primitive tests of this rank's shard
     step(stats_p)
@@ -212,14 +223,14 @@ def main():
     mine = dict(zip(keys, mine.tolist()))
     rays_frame = tot["closest_rays"] + tot["shadow_rays"]
 
-    for _ in range(args.warmup):
-        step(shard_p)
+    for i in range(args.warmup):
+        step(shard_ps[i % pipe], i % pipe)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(shard_p)
+    for i in range(args.steps):
+        step(shard_ps[i % pipe], i % pipe)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -229,7 +240,14 @@ def main():
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
 
-    path_ms, total_ms = r.frame_times(args.steps)
+    # roofline.kernel_ms: the path kernel's own duration per launch.  Frames in flight overlap, so
+    # a pipelined frame's HIP-event span also holds its wait for the other frame's blocks; time a
+    # few frames one at a time on one stream instead (untimed, after the timed region).
+    serial = 3
+    for _ in range(serial):
+        r.render_device(shard_p, (frames[0] if world == 1 else fgs[0].shard).data_ptr(), sptr)
+    torch.cuda.synchronize()
+    path_ms, total_ms = r.frame_times(serial)
     frame_check = None
     if args.check_frame:
         step(shard_p)  # assemble one more frame, then compare it with a one-shot whole frame
@@ -289,7 +307,8 @@ def main():
                                + (f", roughness {args.roughness:g}" if args.roughness else "")
                                + (f", {args.light_spp} quad-light samples" if args.light_spp > 1 else ""),
                    "scene": args.scene, "tris": args.tris if args.scene == "synthetic" else 0, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
-                   "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else "")},
+                   "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                   "frames_in_flight": pipe},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),

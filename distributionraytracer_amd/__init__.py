@@ -222,8 +222,9 @@ class Renderer:
         return self
 
     def frame_params(self, seed=1, max_depth=4, roughness=0.0, shard=0, n_shards=1, tile=16, stats=False,
-                     light_spp=1, progressive_frame=0):
+                     light_spp=1, progressive_frame=0, slot=0):
         p = DrtFrameParams()
+        p.slot = slot
         p.light_spp = light_spp
         p.progressive_frame = progressive_frame
         p.seed = seed

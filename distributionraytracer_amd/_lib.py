@@ -42,7 +42,7 @@ class DrtCamera(C.Structure):
 class DrtFrameParams(C.Structure):
     _fields_ = [("seed", C.c_uint32), ("max_depth", C.c_int32), ("roughness", C.c_float), ("shard", C.c_int32),
                 ("n_shards", C.c_int32), ("tile", C.c_int32), ("flags", C.c_int32), ("light_spp", C.c_int32),
-                ("progressive_frame", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("progressive_frame", C.c_int32), ("slot", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 class DrtFrameStats(C.Structure):

@@ -91,6 +91,8 @@ struct drt_ctx {
   int gmacro_shift = 0, gmacro_dim[3] = {0, 0, 0}, gmacro_words = 0;
   // frame scratch
   DevBuf d_samples, d_frame, d_stats, d_rays, d_out, d_counter;
+  DevBuf d_samples1, d_stats1, d_counter1;  // frame scratch of slot 1 (drt_frame_params.slot)
+  int stats_slot = 0;                       // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
   // batched queries: streaming-query records, primitive results, timing of the last call
@@ -527,13 +529,19 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   rc = scene_args(c, c->accel, S);
   if (rc) return rc;
   DRT_HIP(c, hipSetDevice(c->device));
-  DRT_HIP(c, c->d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.n_slots)));
-  DRT_HIP(c, c->d_stats.ensure(sizeof(unsigned long long) * ST_COUNT));
+  // frames on different scratch slots may run concurrently on different streams
+  const int slot = p->slot & 1;
+  DevBuf& d_samples = slot ? c->d_samples1 : c->d_samples;
+  DevBuf& d_stats = slot ? c->d_stats1 : c->d_stats;
+  DevBuf& d_counter = slot ? c->d_counter1 : c->d_counter;
+  c->stats_slot = slot;
+  DRT_HIP(c, d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.n_slots)));
+  DRT_HIP(c, d_stats.ensure(sizeof(unsigned long long) * ST_COUNT));
   const bool stats = (p->flags & DRT_FRAME_STATS) != 0;
   c->stats_valid = stats;
-  if (stats) DRT_HIP(c, hipMemsetAsync(c->d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
-  P.F.samples = c->d_samples.as<float4>();
-  P.F.stats = c->d_stats.as<unsigned long long>();
+  if (stats) DRT_HIP(c, hipMemsetAsync(d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+  P.F.samples = d_samples.as<float4>();
+  P.F.stats = d_stats.as<unsigned long long>();
   P.R.samples = P.F.samples;
   P.R.full_frame = full_frame ? 1 : 0;
   P.R.out = d_out;
@@ -542,9 +550,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   DRT_HIP(c, hipEventRecord(ev[0], st));
   const bool persistent = P.persistent;
   if (persistent) {
-    DRT_HIP(c, c->d_counter.ensure(1024));
-    DRT_HIP(c, hipMemsetAsync(c->d_counter.p, 0, 1024, st));  // 8 partition counters, 64 B apart
-    P.F.work_counter = c->d_counter.as<unsigned int>();
+    DRT_HIP(c, d_counter.ensure(1024));
+    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));  // 8 partition counters, 64 B apart
+    P.F.work_counter = d_counter.as<unsigned int>();
     P.F.part_items = (uint32_t)((P.F.n_items + 7) / 8);
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
     P.F.process_min = env_int("DRT_PROCESS_MIN", 24);
@@ -644,7 +652,7 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
     c->last.render_ms = ms_all;
     if (c->stats_valid) {
       unsigned long long s[ST_COUNT];
-      DRT_HIP(c, hipMemcpy(s, c->d_stats.p, sizeof(s), hipMemcpyDeviceToHost));
+      DRT_HIP(c, hipMemcpy(s, (c->stats_slot ? c->d_stats1 : c->d_stats).p, sizeof(s), hipMemcpyDeviceToHost));
       c->last.closest_rays = s[ST_CLOSEST]; c->last.shadow_rays = s[ST_SHADOW];
       c->last.closest_inner = s[ST_C_INNER]; c->last.closest_leaf = s[ST_C_LEAF];
       c->last.shadow_inner = s[ST_S_INNER]; c->last.shadow_leaf = s[ST_S_LEAF];

@@ -127,7 +127,8 @@ typedef struct {
   uint32_t seed;       /* keyed-RNG seed                                                */
   int32_t max_depth;   /* MAX_DEPTH (main.cpp:34) = 4                                   */
   float roughness;     /* roughness_param (main.cpp:507) = 0                            */
-  int32_t shard;       /* this rank's shard: tiles t with t % n_shards == shard        */
+  int32_t shard;       /* this rank's shard: the tiles at dealing positions p with
+                          p % n_shards == shard (sharding.py: row ty rotated by ty tiles)  */
   int32_t n_shards;    /* 1 = whole frame                                               */
   int32_t tile;        /* tile edge in pixels (0 -> 16)                                 */
   int32_t flags;       /* DRT_FRAME_STATS: count rays / node visits / prim tests        */
@@ -138,7 +139,9 @@ typedef struct {
                           lerped into the output with weight 1/n (n > 1: the output buffer is
                           read, so pass the previous frame back); n >= MAX_SAMPLES (10000)
                           leaves the output untouched (main.cpp:537)                     */
-  int32_t reserved[3];
+  int32_t slot;        /* frame scratch slot, 0 or 1: frames on different slots of one
+                          context may run concurrently on different streams (pipelining) */
+  int32_t reserved[2];
 } drt_frame_params;
 
 typedef struct {

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--shards", default="1,2,4,8")
+    ap.add_argument("--pipe", type=int, default=1, help="frames in flight (bench.py --frames-in-flight)")
     args = ap.parse_args()
 
     import torch
@@ -40,22 +41,24 @@ def main():
     scene.build()
     r = drt.Renderer(0)
     r.upload(scene)
-    stream = torch.cuda.current_stream().cuda_stream
-    out = {"tris": args.tris, "res": args.res, "spp": args.spp, "per_shard": {}}
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.pipe - 1)]
+    out = {"tris": args.tris, "res": args.res, "spp": args.spp, "pipe": args.pipe, "per_shard": {}}
     t1 = None
     for n in (int(x) for x in args.shards.split(",")):
         worst = 0.0
         rec = {}
         for shard in sorted({0, n - 1}):
-            p = r.frame_params(seed=1, shard=shard, n_shards=n)
-            _, floats = r.shard_layout(p)
-            buf = torch.empty(floats, dtype=torch.float32, device="cuda")
-            for _ in range(2):
-                r.render_device(p, buf.data_ptr(), stream)
+            ps = [r.frame_params(seed=1, shard=shard, n_shards=n, slot=j) for j in range(args.pipe)]
+            _, floats = r.shard_layout(ps[0])
+            bufs = [torch.empty(floats, dtype=torch.float32, device="cuda") for _ in range(args.pipe)]
+            for i in range(2):
+                j = i % args.pipe
+                r.render_device(ps[j], bufs[j].data_ptr(), streams[j].cuda_stream)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(args.steps):
-                r.render_device(p, buf.data_ptr(), stream)
+            for i in range(args.steps):
+                j = i % args.pipe
+                r.render_device(ps[j], bufs[j].data_ptr(), streams[j].cuda_stream)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) / args.steps * 1e3
             path_ms, _ = r.frame_times(args.steps)
