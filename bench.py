@@ -127,9 +127,10 @@ def main():
     ap.add_argument("--ks", type=float, default=0.5, help="material Ks (0: no mirror bounces; diagnostics)")
     ap.add_argument("--check-frame", action="store_true",
                     help="after timing, rank 0 checks the assembled frame against a whole-frame render (bitwise)")
-    ap.add_argument("--frames-in-flight", type=int, default=2, choices=[1, 2],
-                    help="frames pipelined on separate streams and scratch slots (2: a frame's start overlaps "
-                         "the previous frame's tail)")
+    ap.add_argument("--frames-in-flight", type=int, default=0, choices=[0, 1, 2, 3, 4],
+                    help="frames pipelined on separate streams and scratch slots, so that a frame's start "
+                         "overlaps the previous frame's tail (0: 2 on one GPU, 3 on several, where a "
+                         "rank's shard is short and the tail a larger share of it)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
@@ -179,7 +180,7 @@ def main():
     sptr = stream.cuda_stream
 
     fkw = {"max_depth": args.max_depth, "roughness": args.roughness, "light_spp": args.light_spp}
-    pipe = args.frames_in_flight
+    pipe = args.frames_in_flight or (3 if world >= 2 else 2)
     shard_ps = [r.frame_params(seed=args.seed, shard=rank, n_shards=world, slot=j, **fkw) for j in range(pipe)]
     shard_p = shard_ps[0]
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
@@ -326,8 +327,9 @@ def main():
         "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
                                          tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3),
                      "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3),
+                     # BVH leaf block only (the Grid stepper has no separate leaf block)
                      "leaf_block": round((tot["closest_leaf"] + tot["shadow_leaf"]) /
-                                         max(1.0, 64 * tot["wave_leaf_iters"]), 3)},
+                                         (64 * tot["wave_leaf_iters"]), 3) if tot["wave_leaf_iters"] else None},
         # traversal-stack pushes per ray and the share that went past the LDS part (scratch)
         "stack": {"pushes_per_ray": round(tot["stack_pushes"] / max(1.0, rays_frame), 2),
                   "spill_frac": round(tot["stack_spills"] / max(1.0, tot["stack_pushes"]), 4)},

@@ -90,9 +90,11 @@ struct drt_ctx {
   DevBuf d_cell_start, d_cell_objs, d_macro, d_cell_recs;
   int gmacro_shift = 0, gmacro_dim[3] = {0, 0, 0}, gmacro_words = 0;
   // frame scratch
-  DevBuf d_samples, d_frame, d_stats, d_rays, d_out, d_counter;
-  DevBuf d_samples1, d_stats1, d_counter1;  // frame scratch of slot 1 (drt_frame_params.slot)
-  int stats_slot = 0;                       // slot of the last frame (drt_get_stats reads its counters)
+  DevBuf d_frame, d_rays, d_out, d_counter;
+  // frame scratch per slot (drt_frame_params.slot): frames on different slots may be in flight
+  // together on different streams
+  DevBuf d_samples_s[DRT_FRAME_SLOTS], d_stats_s[DRT_FRAME_SLOTS], d_counter_s[DRT_FRAME_SLOTS];
+  int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
   // batched queries: streaming-query records, primitive results, timing of the last call
@@ -530,10 +532,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   if (rc) return rc;
   DRT_HIP(c, hipSetDevice(c->device));
   // frames on different scratch slots may run concurrently on different streams
-  const int slot = p->slot & 1;
-  DevBuf& d_samples = slot ? c->d_samples1 : c->d_samples;
-  DevBuf& d_stats = slot ? c->d_stats1 : c->d_stats;
-  DevBuf& d_counter = slot ? c->d_counter1 : c->d_counter;
+  if (p->slot < 0 || p->slot >= DRT_FRAME_SLOTS) DRT_FAIL(c, DRT_E_INVALID, "frame slot out of range");
+  const int slot = p->slot;
+  DevBuf& d_samples = c->d_samples_s[slot];
+  DevBuf& d_stats = c->d_stats_s[slot];
+  DevBuf& d_counter = c->d_counter_s[slot];
   c->stats_slot = slot;
   DRT_HIP(c, d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.n_slots)));
   DRT_HIP(c, d_stats.ensure(sizeof(unsigned long long) * ST_COUNT));
@@ -652,7 +655,7 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
     c->last.render_ms = ms_all;
     if (c->stats_valid) {
       unsigned long long s[ST_COUNT];
-      DRT_HIP(c, hipMemcpy(s, (c->stats_slot ? c->d_stats1 : c->d_stats).p, sizeof(s), hipMemcpyDeviceToHost));
+      DRT_HIP(c, hipMemcpy(s, c->d_stats_s[c->stats_slot].p, sizeof(s), hipMemcpyDeviceToHost));
       c->last.closest_rays = s[ST_CLOSEST]; c->last.shadow_rays = s[ST_SHADOW];
       c->last.closest_inner = s[ST_C_INNER]; c->last.closest_leaf = s[ST_C_LEAF];
       c->last.shadow_inner = s[ST_S_INNER]; c->last.shadow_leaf = s[ST_S_LEAF];

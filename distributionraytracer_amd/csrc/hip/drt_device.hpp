@@ -215,6 +215,24 @@ __device__ __forceinline__ bool hit_box(const float4& q0, const float4& q1, cons
   return false;
 }
 
+// hit_triangle without its early exits: every lane computes u, v and t and the three tests
+// are combined with non-short-circuit ands.  Same operations in the same order, so identical
+// results (a NaN u or v passes both, as in the reference's ||-chains); t is written always and
+// meaningful only when the test returns true.
+__device__ __forceinline__ bool hit_triangle_sel(const float4& q0, const float4& q1, const float4& q2, const RayP& r,
+                                                 float& t) {
+  V3 v0 = mk(q0.x, q0.y, q0.z), e1 = mk(q1.x, q1.y, q1.z), e2 = mk(q2.x, q2.y, q2.z);
+  V3 h = cross(r.d, e2);
+  float a = dot(e1, h);
+  float f = 1.0f / a;
+  V3 s = sub(r.o, v0);
+  float u = f * dot(s, h);
+  V3 q = cross(s, e1);
+  float v = f * dot(r.d, q);
+  t = f * dot(e2, q);
+  return !(u < 0.0f || u > 1.0f) & !(v < 0.0f || u + v > 1.0f) & (t >= kEpsF);
+}
+
 // Object::hit on an already loaded record (q2 is only read for triangles).
 template <bool TRI_ONLY>
 __device__ __forceinline__ bool hit_prim_rec(const float4& q0, const float4& q1, const float4& q2, const RayP& r,

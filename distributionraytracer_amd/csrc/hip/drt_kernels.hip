@@ -819,9 +819,6 @@ __device__ __forceinline__ bool grid_init(const SceneArgs& S, Lane& L) {
 // One cell of Grid::Traverse (grid.cpp:247-306 closest, :309-358 shadow): the cell's objects in
 // insertion order (shadow: any t < |d| ends the query), then the DDA step — closest hits end
 // when best.t < t_next of the stepped axis, leaving the grid is a miss (even with a farther hit).
-// One cell of Grid::Traverse (grid.cpp:247-306 closest, :309-358 shadow): the cell's objects in
-// insertion order (shadow: any t < |d| ends the query), then the DDA step — closest hits end
-// when best.t < t_next of the stepped axis, leaving the grid is a miss (even with a farther hit).
 // (Measured alternative, kept out: one memory round trip per iteration — the cell range, or two
 // objects with the next cell's range prefetched speculatively — 6-17 % slower than a whole cell
 // per iteration.)
@@ -836,17 +833,18 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   const uint32_t b = S.cell_start[cidx], e = S.cell_start[cidx + 1];
   // the cell's objects in insertion order, two inline records (drt_upload_grid) per round trip
   bool done = false;
+  // triangle scenes: the test and the hit update as selects, no exec-mask branches per object
+  // (+1.3 % Mrays/s on the Grid; the same test in the BVH leaf block measured -1.7 %)
   auto test = [&](const float4& p0, const float4& p1, const float4& p2) {
     if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
     float t;
-    if (hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t)) {
-      if (shadow) {
-        if (t < L.thr) done = true;
-      } else if (t < L.best_t) {
-        L.best_t = t;
-        L.best_prim = __float_as_uint(p2.w);
-      }
-    }
+    bool h;
+    if (TRI_ONLY) h = hit_triangle_sel(p0, p1, p2, L.q, t);
+    else h = hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t);
+    const bool nearer = h & !shadow & (t < L.best_t);
+    done = done | (h & shadow & (t < L.thr));
+    L.best_t = nearer ? t : L.best_t;
+    L.best_prim = nearer ? __float_as_uint(p2.w) : L.best_prim;
   };
   for (uint32_t q = b; q < e; q += 2) {
     const float4* r = S.cell_recs + 3 * (size_t)q;

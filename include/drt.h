@@ -41,6 +41,7 @@ extern "C" {
 #endif
 
 #define DRT_ABI_VERSION 1
+#define DRT_FRAME_SLOTS 4 /* drt_frame_params.slot: 0 .. DRT_FRAME_SLOTS-1 */
 
 typedef enum {
   DRT_OK = 0,
@@ -139,8 +140,9 @@ typedef struct {
                           lerped into the output with weight 1/n (n > 1: the output buffer is
                           read, so pass the previous frame back); n >= MAX_SAMPLES (10000)
                           leaves the output untouched (main.cpp:537)                     */
-  int32_t slot;        /* frame scratch slot, 0 or 1: frames on different slots of one
-                          context may run concurrently on different streams (pipelining) */
+  int32_t slot;        /* frame scratch slot, 0 .. DRT_FRAME_SLOTS-1: frames on different
+                          slots of one context may run concurrently on different streams
+                          (pipelining); other values are DRT_E_INVALID                    */
   int32_t reserved[2];
 } drt_frame_params;
 

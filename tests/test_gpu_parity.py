@@ -371,20 +371,23 @@ def test_no_lights_and_deepest_recursion_match_oracle(drt, oracle_mod, renderer,
         compare_images(img, ref)
 
 
-def test_pipelined_slots_match_sequential_frame(drt, renderer, tmp_path):
-    """Two frames in flight (scratch slots 0 and 1, one stream each, bench.py --frames-in-flight 2)
-    give the frame a lone render gives, bit for bit."""
+@pytest.mark.parametrize("pipe", [2, 4])
+def test_pipelined_slots_match_sequential_frame(drt, renderer, tmp_path, pipe):
+    """Frames in flight (scratch slots 0 .. pipe-1, one stream each, bench.py --frames-in-flight)
+    give the frame a lone render gives, bit for bit; a slot outside DRT_FRAME_SLOTS is refused."""
     import torch
 
     p = sg.write(tmp_path, "s.p3f", sg.synthetic_scene_text(20000, res=(64, 48), spp=16))
     s = drt.Scene.load_p3f(p)
     renderer.upload(s)
     whole = renderer.render(seed=21)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    outs = [torch.zeros((48, 64, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
-    for i in range(6):
-        j = i % 2
+    streams = [torch.cuda.Stream() for _ in range(pipe)]
+    outs = [torch.zeros((48, 64, 3), dtype=torch.float32, device="cuda") for _ in range(pipe)]
+    for i in range(3 * pipe):
+        j = i % pipe
         renderer.render_device(renderer.frame_params(seed=21, slot=j), outs[j].data_ptr(), streams[j].cuda_stream)
     torch.cuda.synchronize()
     for o in outs:
         np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), whole.view(np.uint32))
+    with pytest.raises(RuntimeError, match="slot"):
+        renderer.render_device(renderer.frame_params(seed=21, slot=4), outs[0].data_ptr(), streams[0].cuda_stream)
