@@ -1713,7 +1713,9 @@ static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStrea
 }
 template <bool T, bool ST, int M, int A>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
-  if (A == ACC_BVH && F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);  // register budget (waves/SIMD)
+  // register budget (waves/SIMD); DRT_WAVES=7 measured slower on both accelerators (Grid at 7 / 8
+  // waves: 523 / 446 against 590 Mrays/s at 6)
+  if (F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);
   else launch_persistent_w<T, ST, M, 6, A>(S, F, st);
 }
 template <bool T, bool ST, int A>
