@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--pipe", type=int, default=1, help="frames in flight (bench.py --frames-in-flight)")
+    ap.add_argument("--all-shards", action="store_true", help="time every shard, not just the first and last")
+    ap.add_argument("--tile", type=int, default=16, help="tile edge in pixels (drt_frame_params.tile)")
     args = ap.parse_args()
 
     import torch
@@ -42,13 +44,13 @@ def main():
     r = drt.Renderer(0)
     r.upload(scene)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(args.pipe - 1)]
-    out = {"tris": args.tris, "res": args.res, "spp": args.spp, "pipe": args.pipe, "per_shard": {}}
+    out = {"tris": args.tris, "res": args.res, "spp": args.spp, "pipe": args.pipe, "tile": args.tile, "per_shard": {}}
     t1 = None
     for n in (int(x) for x in args.shards.split(",")):
         worst = 0.0
         rec = {}
-        for shard in sorted({0, n - 1}):
-            ps = [r.frame_params(seed=1, shard=shard, n_shards=n, slot=j) for j in range(args.pipe)]
+        for shard in (range(n) if args.all_shards else sorted({0, n - 1})):
+            ps = [r.frame_params(seed=1, shard=shard, n_shards=n, slot=j, tile=args.tile) for j in range(args.pipe)]
             _, floats = r.shard_layout(ps[0])
             bufs = [torch.empty(floats, dtype=torch.float32, device="cuda") for _ in range(args.pipe)]
             for i in range(2):
