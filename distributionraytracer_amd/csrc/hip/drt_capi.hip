@@ -14,6 +14,7 @@
 
 namespace drt {
 void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_only, bool stats, hipStream_t st);
+void launch_shuffle(const FrameArgs& F, int res_x, int res_y, uint8_t* perm, hipStream_t st);
 void launch_reduce(const ReduceArgs& A, hipStream_t st);
 void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, int n_tiles, int n_shards,
                     int tiles_per_shard, int res_x, int res_y, hipStream_t st);
@@ -93,7 +94,7 @@ struct drt_ctx {
   DevBuf d_frame, d_rays, d_out, d_counter;
   // frame scratch per slot (drt_frame_params.slot): frames on different slots may be in flight
   // together on different streams
-  DevBuf d_samples_s[DRT_FRAME_SLOTS], d_stats_s[DRT_FRAME_SLOTS], d_counter_s[DRT_FRAME_SLOTS];
+  DevBuf d_samples_s[DRT_FRAME_SLOTS], d_stats_s[DRT_FRAME_SLOTS], d_counter_s[DRT_FRAME_SLOTS], d_perm_s[DRT_FRAME_SLOTS];
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
@@ -548,6 +549,16 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   P.R.samples = P.F.samples;
   P.R.full_frame = full_frame ? 1 : 0;
   P.R.out = d_out;
+  // per-pixel sample shuffle, once per pixel instead of once per sample (spp < 2: no shuffle); ahead
+  // of the frame's first event, so that the path-kernel time is the persistent kernel's own
+  const bool shuffled = P.F.mode == MODE_AA || (P.F.mode == MODE_SEQ && P.F.spp > 0);
+  if (P.persistent && shuffled && P.F.spp >= 2 && P.F.spp <= 256 && P.F.n_items && env_int("DRT_PERM", 1)) {
+    DevBuf& d_perm = c->d_perm_s[slot];
+    DRT_HIP(c, d_perm.ensure((size_t)P.F.n_my_tiles * P.F.tile * P.F.tile * P.F.spp));
+    launch_shuffle(P.F, c->cam.res_x, c->cam.res_y, d_perm.as<uint8_t>(), st);
+    P.F.perm = d_perm.as<uint8_t>();
+    DRT_HIP(c, hipGetLastError());
+  }
   hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
   c->frames++;
   DRT_HIP(c, hipEventRecord(ev[0], st));

@@ -572,22 +572,54 @@ __device__ __forceinline__ Item decode_item(const FrameArgs& F, int res_x, int r
 // Pixel jitter r[p] and the shuffled light sample s[p] of sample p, straight from the keyed
 // stream: r uses calls 4p, 4p+1; s uses 4q+2, 4q+3 of the sample q that the Fisher-Yates pass
 // (calls 4spp .. 5spp-2) moved to slot p.  Tracking slot p backwards through the swaps gives q.
-__device__ __forceinline__ void sample_prologue(const FrameArgs& F, uint32_t pmix, int p, float& rx, float& ry,
-                                                float& sx, float& sy) {
-  const int n = F.n_sqrt;
+__device__ __forceinline__ int shuffle_source(const FrameArgs& F, uint32_t pmix, int p) {
   const int spp = (int)F.spp;
-  float ex = (float)keyed_rand(F.seed, pmix, 4u * p) / 32767.0f;
-  float ey = (float)keyed_rand(F.seed, pmix, 4u * p + 1u) / 32767.0f;
-  rx = ((float)(p % n) + ex) / (float)n;
-  ry = ((float)(p / n) + ey) / (float)n;
   int pos = p;
   for (int i = 1; i < spp; i++) {
     int jj = keyed_rand(F.seed, pmix, 4u * spp + (uint32_t)(spp - 1 - i)) % (i + 1);
     if (pos == i) pos = jj;
     else if (pos == jj) pos = i;
   }
+  return pos;
+}
+__device__ __forceinline__ void sample_prologue_at(const FrameArgs& F, uint32_t pmix, int p, int pos, float& rx,
+                                                   float& ry, float& sx, float& sy) {
+  const int n = F.n_sqrt;
+  float ex = (float)keyed_rand(F.seed, pmix, 4u * p) / 32767.0f;
+  float ey = (float)keyed_rand(F.seed, pmix, 4u * p + 1u) / 32767.0f;
+  rx = ((float)(p % n) + ex) / (float)n;
+  ry = ((float)(p / n) + ey) / (float)n;
   sx = (float)keyed_rand(F.seed, pmix, 4u * pos + 2u) / 32767.0f;
   sy = (float)keyed_rand(F.seed, pmix, 4u * pos + 3u) / 32767.0f;
+}
+__device__ __forceinline__ void sample_prologue(const FrameArgs& F, uint32_t pmix, int p, float& rx, float& ry,
+                                                float& sx, float& sy) {
+  sample_prologue_at(F, pmix, p, shuffle_source(F, pmix, p), rx, ry, sx, sy);
+}
+
+// The whole Fisher-Yates pass of main.cpp:642-648 once per pixel, forward, on an LDS copy of
+// the slot array: perm[pixel * spp + p] = the sample whose light sample ends in slot p — what
+// shuffle_source finds for one slot by walking the spp - 1 swaps backwards.  The path kernel
+// then reads one byte per sample instead of hashing spp - 1 keyed draws.
+constexpr int kShuffleBlock = 64;
+__global__ void __launch_bounds__(kShuffleBlock) shuffle_kernel(FrameArgs F, int res_x, int res_y, uint8_t* perm) {
+  __shared__ uint8_t a[256 * kShuffleBlock];  // a[k * kShuffleBlock + thread]
+  const uint32_t px = blockIdx.x * kShuffleBlock + threadIdx.x;
+  const uint32_t n_px = (uint32_t)F.n_my_tiles * F.tile * F.tile;
+  if (px >= n_px) return;
+  const Item it = decode_item(F, res_x, res_y, px, 1);
+  const int spp = (int)F.spp;
+  uint8_t* o = perm + (size_t)px * spp;
+  if (!it.valid) return;  // padding of a partial tile: never read
+  const uint32_t pmix = (uint32_t)(it.y * res_x + it.x) * 0x9E3779B9u;
+  for (int k = 0; k < spp; k++) a[k * kShuffleBlock + threadIdx.x] = (uint8_t)k;
+  for (int i = spp - 1; i >= 1; i--) {  // j = rand() % (i + 1); swap(s[i], s[j])
+    const int j = keyed_rand(F.seed, pmix, 4u * spp + (uint32_t)(spp - 1 - i)) % (i + 1);
+    const uint8_t t = a[i * kShuffleBlock + threadIdx.x];
+    a[i * kShuffleBlock + threadIdx.x] = a[j * kShuffleBlock + threadIdx.x];
+    a[j * kShuffleBlock + threadIdx.x] = t;
+  }
+  for (int k = 0; k < spp; k++) o[k] = a[k * kShuffleBlock + threadIdx.x];
 }
 
 template <bool STATS>
@@ -1256,7 +1288,8 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
   RayP r;
   if (F.spp > 0) {
     float rx, ry, sx, sy;
-    sample_prologue(F, L.pmix, (int)L.smp, rx, ry, sx, sy);
+    const int pos = F.perm ? (int)F.perm[(size_t)L.item * F.spp + L.smp] : shuffle_source(F, L.pmix, (int)L.smp);
+    sample_prologue_at(F, L.pmix, (int)L.smp, pos, rx, ry, sx, sy);
     const float px = (float)it.x + rx, py = (float)it.y + ry;
     if (F.dof) {
       KRng rng{F.seed, L.pmix, L.rk};
@@ -1329,7 +1362,8 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
   if (MODE == MODE_AA) {
     const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     float rx, ry, sx, sy;
-    sample_prologue(F, pmix, it.sub, rx, ry, sx, sy);
+    const int pos = F.perm ? (int)F.perm[item] : shuffle_source(F, pmix, it.sub);  // item = pixel * spp + sub
+    sample_prologue_at(F, pmix, it.sub, pos, rx, ry, sx, sy);
     r = primary_ray(S, (float)it.x + rx, (float)it.y + ry);
     L.ls = mk(sx, sy, 0.0f);
   } else if (MODE == MODE_WHITTED_QUAD) {
@@ -1749,6 +1783,12 @@ void launch_path(const SceneArgs& S, const FrameArgs& F, int accel, bool tri_onl
   if (accel == ACC_BVH) { if (tri_only) launch_path_t<ACC_BVH, true>(S, F, stats, st); else launch_path_t<ACC_BVH, false>(S, F, stats, st); }
   else if (accel == ACC_GRID) { if (tri_only) launch_path_t<ACC_GRID, true>(S, F, stats, st); else launch_path_t<ACC_GRID, false>(S, F, stats, st); }
   else { if (tri_only) launch_path_t<ACC_NONE, true>(S, F, stats, st); else launch_path_t<ACC_NONE, false>(S, F, stats, st); }
+}
+
+void launch_shuffle(const FrameArgs& F, int res_x, int res_y, uint8_t* perm, hipStream_t st) {
+  const uint32_t n_px = (uint32_t)F.n_my_tiles * F.tile * F.tile;
+  hipLaunchKernelGGL(shuffle_kernel, dim3((n_px + kShuffleBlock - 1) / kShuffleBlock), dim3(kShuffleBlock), 0, st, F,
+                     res_x, res_y, perm);
 }
 
 void launch_reduce(const ReduceArgs& A, hipStream_t st) {

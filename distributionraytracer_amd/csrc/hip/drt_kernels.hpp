@@ -94,6 +94,7 @@ struct FrameArgs {
   int process_min;             // persistent kernel: shade once this many lanes have a result
   int waves;                   // persistent kernel: register budget (waves per SIMD: 6 or 7)
   uint32_t part_items;         // persistent kernel: items per XCD work partition (ceil(n_items / 8))
+  const uint8_t* perm;         // persistent kernel, AA / in-order frames: shuffle_kernel's slot -> sample map
 };
 
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.

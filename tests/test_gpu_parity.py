@@ -129,6 +129,11 @@ RENDER_CASES = {
                                                           focal=1.5), {"roughness": 0.1, "max_depth": 8}),
     # oversized BVH leaves (>= 31 objects: count-31 descriptors, count in the first record)
     "big_leaf_bvh": (lambda: sg.mixed_scene_text(res=(32, 24), spp=4, accel="bvh", cluster=40), {}),
+    # the per-pixel shuffle prepass at its byte limit (spp 256), and past it (the kernel's own walk)
+    "aa_spp256_bvh": (lambda: sg.mixed_scene_text(res=(8, 6), spp=256, accel="bvh", n_tris=60), {}),
+    "aa_spp289_bvh": (lambda: sg.mixed_scene_text(res=(6, 5), spp=289, accel="bvh", n_tris=60), {}),
+    "dof_spp256_bvh": (lambda: sg.mixed_scene_text(res=(6, 5), spp=256, accel="bvh", n_tris=60, aperture=8.0,
+                                                   focal=1.5), {}),
     "big_leaf_dof_bvh": (lambda: sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", cluster=40, aperture=8.0,
                                                      focal=1.5), {}),
 }
@@ -391,3 +396,17 @@ def test_pipelined_slots_match_sequential_frame(drt, renderer, tmp_path, pipe):
         np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), whole.view(np.uint32))
     with pytest.raises(RuntimeError, match="slot"):
         renderer.render_device(renderer.frame_params(seed=21, slot=4), outs[0].data_ptr(), streams[0].cuda_stream)
+
+
+@pytest.mark.parametrize("aperture", [0.0, 8.0])
+def test_shuffle_prepass_matches_in_kernel_walk(drt, renderer, tmp_path, aperture, monkeypatch):
+    """The per-pixel Fisher-Yates prepass (shuffle_kernel) and the kernel's own backward walk over
+    the swaps (DRT_PERM=0) give the same frame, bit for bit (AA and in-order DoF frames)."""
+    p = sg.write(tmp_path, "s.p3f", sg.mixed_scene_text(res=(40, 24), spp=16, accel="bvh", n_tris=80,
+                                                        aperture=aperture, focal=1.5))
+    renderer.upload(drt.Scene.load_p3f(p))
+    with_perm = renderer.render(seed=5)
+    monkeypatch.setenv("DRT_PERM", "0")
+    walk = renderer.render(seed=5)
+    np.testing.assert_array_equal(with_perm.view(np.uint32), walk.view(np.uint32))
+

@@ -12,7 +12,7 @@ run() {  # name, bench args...
   echo "$name rc=$rc $(cut -c1-160 $OUT/cfg_$name.json)"
   return $rc
 }
-run C2_balls_low_bvh_512_16spp --scene balls_low --res 512 --spp 16 &&
+run C2_balls_low_bvh_512_16spp --scene balls_low --res 512 --spp 16 --steps 30 &&  # 1 ms frames: more steps
 run C3_tri100k_512_64spp_soft4 --tris 100000 --res 512 --spp 64 --light-spp 4 &&
 run headline_tri1M_512_64spp &&
 run headline_grid --accel grid &&
