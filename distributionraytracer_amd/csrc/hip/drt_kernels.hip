@@ -735,7 +735,8 @@ constexpr uint32_t kNoItem = 0xFFFFFFFFu;
 // LDS traversal-stack entries per thread for a given occupancy target (5 blocks of 256 threads
 // fit 16 entries in 160 KiB; 6-8 blocks need a shorter LDS stack, the rest spills to scratch).
 __host__ __device__ constexpr int lds_cap(int waves) {
-  return (160 * 1024 / (waves * kBlock * 8) - 1) < 16 ? (160 * 1024 / (waves * kBlock * 8) - 1) : 16;
+  // per thread: 160 KiB over waves * 4 SIMDs * 64 lanes, 8 B per entry, whatever the block size
+  return (160 * 1024 / (waves * 256 * 8) - 1) < 16 ? (160 * 1024 / (waves * 256 * 8) - 1) : 16;
 }
 
 // Per-lane state flags, packed into one VGPR: divergent bools kept as separate variables
@@ -755,9 +756,9 @@ struct Lane {
   // query in flight
   RayP q;
   uint32_t cur, best_prim;
-  // traversal-stack pointer as an LDS byte address: spa = depth * 1024 + threadIdx.x * 4 (the
-  // [entry][thread] layout of a 256-thread block), so depth = spa >> 10 and the lane's own
-  // column survives in the low bits — no base address has to stay live across the loop
+  // traversal-stack pointer as an LDS byte address: spa = depth * kRowBytes + threadIdx.x * 4
+  // (the [entry][thread] layout of a kPBlock-thread block), so depth = spa >> kRowShift and the
+  // lane's own column survives in the low bits — no base address has to stay live across the loop
   uint32_t spa;
   float best_t, thr;
   // path (rayTracing call chain)
@@ -939,7 +940,7 @@ __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const R
     L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (in ? LF_TRAV : (shadow ? LF_HIT : 0u));
     return;
   }
-  L.spa &= 1023u;
+  L.spa &= kRowBytes - 1u;
   L.cur = S.root_desc;
   float tmp;
   const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
@@ -972,7 +973,7 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, class LaneT>
 __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
-  constexpr uint32_t kLdsBytes = (uint32_t)CAP * kBlock * 4u;  // desc part; the t part follows
+  constexpr uint32_t kLdsBytes = (uint32_t)CAP * kRowBytes;  // desc part; the t part follows
   uint32_t fl = L.fl;
   const bool shadow = KIND == 0 ? (fl & LF_SHADOW) != 0u : KIND == 2;
   const uint32_t cur = L.cur;
@@ -1029,10 +1030,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       *(LdsU32*)(lds + spa) = pd;
       *(LdsF32*)(lds + kLdsBytes + spa) = pt;
     } else if (both) {
-      ov_desc[(spa >> 10) - CAP] = pd;
-      ov_t[(spa >> 10) - CAP] = pt;
+      ov_desc[(spa >> kRowShift) - CAP] = pd;
+      ov_t[(spa >> kRowShift) - CAP] = pt;
     }
-    L.spa = spa + (both ? 1024u : 0u);
+    L.spa = spa + (both ? kRowBytes : 0u);
     if (STATS && both) {
       C.v[ST_PUSH]++;
       if (spa >= kLdsBytes) C.v[ST_PUSH_SPILL]++;
@@ -1082,10 +1083,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   }
   if (STATS) cyc_leaf += stamp_cycles() - t0;
   if ((fl & (LF_POP | LF_TRAV)) == (LF_POP | LF_TRAV)) {  // bvh.cpp:299-311 / :381-387
-    if (L.spa < 1024u) {
+    if (L.spa < kRowBytes) {
       fl &= ~LF_TRAV;
     } else {
-      const uint32_t spa = L.spa - 1024u;
+      const uint32_t spa = L.spa - kRowBytes;
       L.spa = spa;
       uint32_t pd;
       float pt;
@@ -1093,8 +1094,8 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
         pd = *(LdsU32*)(lds + spa);
         pt = *(LdsF32*)(lds + kLdsBytes + spa);
       } else {
-        pd = ov_desc[(spa >> 10) - CAP];
-        pt = ov_t[(spa >> 10) - CAP];
+        pd = ov_desc[(spa >> kRowShift) - CAP];
+        pt = ov_t[(spa >> kRowShift) - CAP];
       }
       if (shadow || pt < L.best_t) {
         L.cur = pd;
@@ -1378,10 +1379,14 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
   start_query<STATS, ACC>(S, L, r, false, 0.0f, C);
 }
 
+// Block size of path_persistent: kPBlock for the BVH; 256 for the Grid, whose per-block LDS
+// copy of the macro-cell bitmap (16 KiB) has to fit the CU once per block.
+template <int ACC>
+__host__ __device__ constexpr int pblock() { return ACC == ACC_GRID ? 256 : kPBlock; }
+
 template <bool TRI_ONLY, bool STATS, int MODE, int WAVES, int ACC>
-__global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, FrameArgs F) {
+__global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArgs S, FrameArgs F) {
   constexpr int CAP = lds_cap(WAVES);
-  static_assert(kBlock * 4 == 1024, "spa encoding assumes 256-thread blocks");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_bytes[];
   uint32_t ov_desc[kMaxBvhDepth - CAP];
   float ov_t[kMaxBvhDepth - CAP];
@@ -1389,7 +1394,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) path_persistent(SceneArgs S, Fr
   Counters C;
   for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
   if (ACC == ACC_GRID) {  // the macro-cell occupancy bitmap, once per block
-    for (int w = threadIdx.x; w < S.gmacro_words; w += kBlock) ((LdsU32*)lds_bytes)[w] = S.gmacro[w];
+    for (int w = threadIdx.x; w < S.gmacro_words; w += pblock<ACC>()) ((LdsU32*)lds_bytes)[w] = S.gmacro[w];
     __syncthreads();
   }
   Lane L;
@@ -1499,9 +1504,8 @@ struct TLane {
 };
 
 template <bool TRI_ONLY, int KIND, int WAVES, bool STATS>
-__global__ void __launch_bounds__(kBlock, WAVES) trace_stream(SceneArgs S, TraceArgs A) {
+__global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, TraceArgs A) {
   constexpr int CAP = lds_cap(WAVES);
-  static_assert(kBlock * 4 == 1024, "spa encoding assumes 256-thread blocks");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_bytes[];
   uint32_t ov_desc[kMaxBvhDepth - CAP];
   float ov_t[kMaxBvhDepth - CAP];
@@ -1540,7 +1544,7 @@ __global__ void __launch_bounds__(kBlock, WAVES) trace_stream(SceneArgs S, Trace
           L.thr = a.w;
           L.best_t = 3.402823466e+38f;
           L.best_prim = 0xFFFFFFFFu;
-          L.spa &= 1023u;
+          L.spa &= kRowBytes - 1u;
           L.cur = S.root_desc;
           float tmp;
           const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
@@ -1731,19 +1735,20 @@ static void launch_path_t(const SceneArgs& S, const FrameArgs& F, bool stats, hi
 template <bool T, bool ST, int M, int W, int A>
 static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
   // the BVH kernel keeps its traversal stack's top in LDS; the Grid stepper needs none
-  const size_t lds = A == ACC_BVH ? (size_t)lds_cap(W) * kBlock * 8 : kMacroBits / 8;
+  constexpr int B = pblock<A>();
+  const size_t lds = A == ACC_BVH ? (size_t)lds_cap(W) * B * 8 : kMacroBits / 8;
   static int grid = 0;  // resident blocks across the device (per instantiation)
   if (!grid) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_persistent<T, ST, M, W, A>, kBlock,
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)path_persistent<T, ST, M, W, A>, B,
                                                        lds);
     grid = std::max(1, cus) * std::max(1, per_cu);
   }
-  const uint64_t need = (F.n_items + kBlock - 1) / kBlock;
+  const uint64_t need = (F.n_items + B - 1) / B;
   const unsigned blocks = (unsigned)std::min<uint64_t>(need, (uint64_t)grid);
-  hipLaunchKernelGGL((path_persistent<T, ST, M, W, A>), dim3(blocks), dim3(kBlock), lds, st, S, F);
+  hipLaunchKernelGGL((path_persistent<T, ST, M, W, A>), dim3(blocks), dim3(B), lds, st, S, F);
 }
 template <bool T, bool ST, int M, int A>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
@@ -1805,18 +1810,18 @@ void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, in
 
 template <bool T, int K, int W, bool ST>
 static void launch_stream_w(const SceneArgs& S, const TraceArgs& A, hipStream_t st) {
-  const size_t lds = (size_t)lds_cap(W) * kBlock * 8;
+  const size_t lds = (size_t)lds_cap(W) * kPBlock * 8;
   static int grid = 0;  // resident blocks across the device (per instantiation)
   if (!grid) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_stream<T, K, W, ST>, kBlock, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_stream<T, K, W, ST>, kPBlock, lds);
     grid = std::max(1, cus) * std::max(1, per_cu);
   }
-  const uint64_t need = ((uint64_t)A.n + kBlock - 1) / kBlock;
+  const uint64_t need = ((uint64_t)A.n + kPBlock - 1) / kPBlock;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)grid));
-  hipLaunchKernelGGL((trace_stream<T, K, W, ST>), dim3(blocks), dim3(kBlock), lds, st, S, A);
+  hipLaunchKernelGGL((trace_stream<T, K, W, ST>), dim3(blocks), dim3(kPBlock), lds, st, S, A);
 }
 template <bool T, int K, bool ST>
 static void launch_stream_k(const SceneArgs& S, const TraceArgs& A, int waves, hipStream_t st) {

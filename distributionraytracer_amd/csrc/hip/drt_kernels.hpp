@@ -35,6 +35,16 @@ constexpr int kMaxFrames = 16;     // max_depth <= 15
 constexpr int kMaxBvhDepth = 96;   // traversal stack entries (host rejects deeper trees)
 constexpr int kLdsStack = 16;      // traversal stack entries kept in LDS per thread
 constexpr int kBlock = 256;        // path-kernel block size
+#ifndef DRT_PBLOCK
+#define DRT_PBLOCK 256
+#endif
+// Block size of the BVH persistent and streaming kernels.  Their LDS traversal stack is laid out
+// [entry][thread] with one kRowBytes row per entry, and the stack pointer is the LDS byte address
+// depth * kRowBytes + threadIdx.x * 4 (so depth = spa >> kRowShift).
+constexpr int kPBlock = DRT_PBLOCK;
+constexpr uint32_t kRowBytes = (uint32_t)kPBlock * 4u;
+constexpr int kRowShift = kPBlock == 256 ? 10 : (kPBlock == 128 ? 9 : 8);
+static_assert(kPBlock == 256 || kPBlock == 128 || kPBlock == 64, "persistent block: 64, 128 or 256 threads");
 constexpr size_t kMacroBits = 131072;  // Grid macro-cell bitmap budget: 16 KB of LDS per block
 constexpr size_t kPrimPadBytes = 64;  // zeroed tail of the primitive buffer (node_step's slot reads)
 
