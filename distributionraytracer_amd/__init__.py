@@ -252,6 +252,13 @@ class Renderer:
         check(_lib.load().drt_render(self.h, C.byref(p), _fp(out)), self.h, "drt_render")
         return out
 
+    def plan(self, params):
+        """drt_plan_frame: work items, sample slots, mode and kernel choice of a frame (no device work)."""
+        out = _lib.DrtFramePlan()
+        check(_lib.load().drt_plan_frame(self.h, C.byref(params), C.byref(out)), self.h, "drt_plan_frame")
+        return dict(work_items=int(out.work_items), sample_slots=int(out.sample_slots), mode=int(out.mode),
+                    persistent=bool(out.persistent), tiles_in_shard=int(out.tiles_in_shard))
+
     def render_device(self, params, d_out_ptr, stream=None):
         """Asynchronous: shard (or whole frame) into a device pointer on `stream` (int handle)."""
         check(_lib.load().drt_render_device(self.h, C.byref(params), C.c_void_p(d_out_ptr),

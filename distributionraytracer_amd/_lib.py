@@ -57,6 +57,35 @@ class DrtFrameStats(C.Structure):
         return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_}
 
 
+class DrtFramePlan(C.Structure):
+    _fields_ = [("work_items", C.c_uint64), ("sample_slots", C.c_uint64), ("mode", C.c_int32),
+                ("persistent", C.c_int32), ("tiles_in_shard", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
+class DrtLight(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pos", C.c_float * 3), ("e1", C.c_float * 3), ("e2", C.c_float * 3),
+                ("grid_res", C.c_uint32)]
+
+
+class DrtMaterial(C.Structure):
+    _fields_ = [("diff", C.c_float * 3), ("kd", C.c_float), ("spec", C.c_float * 3), ("ks", C.c_float),
+                ("shine", C.c_float), ("refl", C.c_float), ("trans", C.c_float), ("ior", C.c_float)]
+
+
+class DrtPrim(C.Structure):
+    _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("a", C.c_float * 3), ("b", C.c_float * 3),
+                ("c", C.c_float * 3), ("r", C.c_float)]
+
+
+class DrtSceneDesc(C.Structure):
+    """drt_scene_desc (include/drt.h): what drt_upload_scene reads."""
+    _fields_ = [("camera", DrtCamera), ("materials", C.POINTER(DrtMaterial)), ("n_materials", C.c_int32),
+                ("prims", C.POINTER(DrtPrim)), ("n_prims", C.c_int32), ("lights", C.POINTER(DrtLight)),
+                ("n_lights", C.c_int32), ("background", C.c_float * 3), ("accel", C.c_int32), ("spp", C.c_uint32),
+                ("has_skybox", C.c_int32), ("skybox", C.c_void_p * 6), ("sky_w", C.c_int32 * 6),
+                ("sky_h", C.c_int32 * 6), ("sky_bpp", C.c_int32 * 6)]
+
+
 class DrtSceneInfo(C.Structure):
     _fields_ = [("res_x", C.c_int32), ("res_y", C.c_int32), ("spp", C.c_uint32), ("accel", C.c_int32),
                 ("n_objects", C.c_int32), ("n_lights", C.c_int32), ("n_materials", C.c_int32),
@@ -71,11 +100,12 @@ SIGNATURES = {
     "drt_create": (C.c_int, [C.POINTER(_vp), C.POINTER(DrtOptions)]),
     "drt_destroy": (None, [_vp]),
     "drt_last_error": (C.c_char_p, [_vp]),
-    "drt_upload_scene": (C.c_int, [_vp, _vp]),
+    "drt_upload_scene": (C.c_int, [_vp, C.POINTER(DrtSceneDesc)]),
     "drt_upload_bvh": (C.c_int, [_vp, _vp, C.c_uint32, _u32, C.c_uint32]),
     "drt_upload_grid": (C.c_int, [_vp, _i32, _f, _f, _i64, _i32, C.c_int64]),
     "drt_render": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _f]),
     "drt_shard_layout": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _i64, _i64]),
+    "drt_plan_frame": (C.c_int, [_vp, C.POINTER(DrtFrameParams), C.POINTER(DrtFramePlan)]),
     "drt_render_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp]),
     "drt_unshard_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp, _vp]),
     "drt_trace_closest": (C.c_int, [_vp, _f, C.c_int32, _f, _f, _i32]),

@@ -198,65 +198,75 @@ const char* drt_last_error(const drt_ctx* c) { return c ? c->err.c_str() : "null
 
 int drt_upload_scene(drt_ctx* c, const drt_scene_desc* s) {
   if (!c || !s) return DRT_E_INVALID;
+  // Nothing renders against a half-replaced scene: the context's scene and accelerator are
+  // invalid from here until this upload has committed every buffer.
+  c->has_scene = c->has_bvh = c->has_grid = false;
   if (s->camera.res_x <= 0 || s->camera.res_y <= 0) DRT_FAIL(c, DRT_E_INVALID, "camera resolution must be positive");
   if (s->n_prims < 0 || (s->n_prims > 0 && !s->prims)) DRT_FAIL(c, DRT_E_INVALID, "bad primitive array");
   if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) DRT_FAIL(c, DRT_E_INVALID, "bad light array");
   if (s->n_materials < 0 || (s->n_materials > 0 && !s->materials)) DRT_FAIL(c, DRT_E_INVALID, "bad material array");
   if (s->accel < DRT_ACCEL_NONE || s->accel > DRT_ACCEL_BVH) DRT_FAIL(c, DRT_E_INVALID, "bad accel %d", s->accel);
-  DRT_HIP(c, hipSetDevice(c->device));
-  c->cam = s->camera;
-  c->accel = s->accel;
-  c->spp = s->spp;
-  memcpy(c->bg, s->background, sizeof(c->bg));
-  c->lights.assign(s->lights, s->lights + s->n_lights);
-  c->mats.assign(s->materials, s->materials + s->n_materials);
+  for (int i = 0; i < s->n_lights; i++)
+    if (s->lights[i].type != DRT_LIGHT_POINT && s->lights[i].type != DRT_LIGHT_QUAD)
+      DRT_FAIL(c, DRT_E_INVALID, "light %d: bad type %d", i, s->lights[i].type);
+  if (s->has_skybox)
+    for (int f = 0; f < 6; f++)
+      if (!s->skybox[f] || s->sky_w[f] <= 0 || s->sky_h[f] <= 0 || (s->sky_bpp[f] != 3 && s->sky_bpp[f] != 4))
+        DRT_FAIL(c, DRT_E_INVALID, "skybox face %d missing or malformed", f);
   // Objects without a material are UB upstream (m_Material uninitialised); they get the
   // default Material() (scene.h:38) appended at the end of the table.
-  const uint32_t dflt = (uint32_t)c->mats.size();
-  c->mats.push_back(drt_material{{0.2f, 0.2f, 0.2f}, 0.2f, {1.f, 1.f, 1.f}, 0.8f, 20.f, 1.0f, 0.0f, 1.0f});
-  c->n_prims = s->n_prims;
-  c->prims_scene.resize((size_t)s->n_prims);
-  c->tri_only = true;
+  std::vector<drt_material> mats(s->materials, s->materials + s->n_materials);
+  const uint32_t dflt = (uint32_t)mats.size();
+  mats.push_back(drt_material{{0.2f, 0.2f, 0.2f}, 0.2f, {1.f, 1.f, 1.f}, 0.8f, 20.f, 1.0f, 0.0f, 1.0f});
+  std::vector<PrimRecord> prims((size_t)s->n_prims);
+  bool tri_only = true;
   for (int i = 0; i < s->n_prims; i++) {
     const drt_prim& p = s->prims[i];
     if (p.type < 0 || p.type > 3) DRT_FAIL(c, DRT_E_INVALID, "prim %d: bad type %d", i, p.type);
     if (p.material >= s->n_materials) DRT_FAIL(c, DRT_E_INVALID, "prim %d: material %d out of range", i, p.material);
-    if (p.type != DRT_PRIM_TRIANGLE) c->tri_only = false;
-    c->prims_scene[i] = pack_prim(p, p.material < 0 ? dflt : (uint32_t)p.material, (uint32_t)i);
+    if (p.type != DRT_PRIM_TRIANGLE) tri_only = false;
+    prims[i] = pack_prim(p, p.material < 0 ? dflt : (uint32_t)p.material, (uint32_t)i);
   }
-  if (s->n_lights > 0 && !c->lights.empty())
-    for (auto& l : c->lights)
-      if (l.type != DRT_LIGHT_POINT && l.type != DRT_LIGHT_QUAD) DRT_FAIL(c, DRT_E_INVALID, "bad light type");
+  std::vector<drt_light> lights(s->lights, s->lights + s->n_lights);
+  // validated: device buffers next (a failure here leaves the context without a scene)
+  DRT_HIP(c, hipSetDevice(c->device));
   // + 64 B: the BVH node step reads four 16-B slots from a leaf's first record and, for leaves of
   // two or more, two more; the tail slots of the last record must stay inside the allocation
-  DRT_HIP(c, c->d_prims.ensure(sizeof(PrimRecord) * c->prims_scene.size() + kPrimPadBytes));
-  DRT_HIP(c, hipMemset(c->d_prims.p, 0, sizeof(PrimRecord) * c->prims_scene.size() + kPrimPadBytes));
-  DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
-                       hipMemcpyHostToDevice));
-  DRT_HIP(c, c->d_lights.ensure(sizeof(drt_light) * std::max<size_t>(1, c->lights.size())));
-  if (!c->lights.empty())
-    DRT_HIP(c, hipMemcpy(c->d_lights.p, c->lights.data(), sizeof(drt_light) * c->lights.size(), hipMemcpyHostToDevice));
-  DRT_HIP(c, c->d_mats.ensure(sizeof(drt_material) * c->mats.size()));
-  DRT_HIP(c, hipMemcpy(c->d_mats.p, c->mats.data(), sizeof(drt_material) * c->mats.size(), hipMemcpyHostToDevice));
-  c->has_sky = s->has_skybox ? 1 : 0;
+  DRT_HIP(c, c->d_prims.ensure(sizeof(PrimRecord) * prims.size() + kPrimPadBytes));
+  DRT_HIP(c, hipMemset(c->d_prims.p, 0, sizeof(PrimRecord) * prims.size() + kPrimPadBytes));
+  DRT_HIP(c, hipMemcpy(c->d_prims.p, prims.data(), sizeof(PrimRecord) * prims.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_lights.ensure(sizeof(drt_light) * std::max<size_t>(1, lights.size())));
+  if (!lights.empty())
+    DRT_HIP(c, hipMemcpy(c->d_lights.p, lights.data(), sizeof(drt_light) * lights.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_mats.ensure(sizeof(drt_material) * mats.size()));
+  DRT_HIP(c, hipMemcpy(c->d_mats.p, mats.data(), sizeof(drt_material) * mats.size(), hipMemcpyHostToDevice));
   for (int f = 0; f < 6; f++) {
     c->sky_w[f] = c->sky_h[f] = c->sky_bpp[f] = 0;
-    if (!c->has_sky) continue;
-    if (!s->skybox[f] || s->sky_w[f] <= 0 || s->sky_h[f] <= 0 || (s->sky_bpp[f] != 3 && s->sky_bpp[f] != 4))
-      DRT_FAIL(c, DRT_E_INVALID, "skybox face %d missing or malformed", f);
+    if (!s->has_skybox) continue;
     size_t n = (size_t)s->sky_w[f] * s->sky_h[f] * s->sky_bpp[f];
     DRT_HIP(c, c->d_sky[f].ensure(n));
     DRT_HIP(c, hipMemcpy(c->d_sky[f].p, s->skybox[f], n, hipMemcpyHostToDevice));
     c->sky_w[f] = s->sky_w[f]; c->sky_h[f] = s->sky_h[f]; c->sky_bpp[f] = s->sky_bpp[f];
   }
+  // commit
+  c->has_sky = s->has_skybox ? 1 : 0;
+  c->cam = s->camera;
+  c->accel = s->accel;
+  c->spp = s->spp;
+  memcpy(c->bg, s->background, sizeof(c->bg));
+  c->lights = std::move(lights);
+  c->mats = std::move(mats);
+  c->n_prims = s->n_prims;
+  c->prims_scene = std::move(prims);
+  c->tri_only = tri_only;
   c->has_scene = true;
-  c->has_bvh = c->has_grid = false;
   return DRT_OK;
 }
 
 int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, const uint32_t* order, uint32_t n_obj) {
   if (!c || !nodes || n_nodes == 0) return DRT_E_INVALID;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its BVH");
+  c->has_bvh = c->has_grid = false;  // until this upload commits
   if ((int)n_obj != c->n_prims || (n_obj && !order)) DRT_FAIL(c, DRT_E_INVALID, "object_order must cover all %d objects", c->n_prims);
   std::vector<uint8_t> seen(n_obj, 0);
   for (uint32_t i = 0; i < n_obj; i++) {
@@ -334,6 +344,7 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
                     const int32_t* co, int64_t n_refs) {
   if (!c || !dims || !bmin || !bmax || !cs || (n_refs > 0 && !co)) return DRT_E_INVALID;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its grid");
+  c->has_bvh = c->has_grid = false;  // until this upload commits
   // A scene without objects: Grid::Build's widths overflow (float FLT_MAX - -FLT_MAX), the cell
   // counts come out NaN -> INT_MIN and the grid has no cells (grid.cpp:56-67); its box is
   // inverted, so every ray misses it.  Same here with one empty cell under that box.
@@ -505,14 +516,18 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
     F.mode = seq ? MODE_SEQ : MODE_WHITTED_POINT;
     F.nsub = 1;
   }
-  P.persistent = persistent_supported(c->accel, c->gdim) && env_int("DRT_PERSISTENT", 1) != 0;
   const int per_pixel = F.mode == MODE_SEQ ? 1 : F.nsub;  // work items per pixel
+  F.n_items = (uint64_t)F.n_my_tiles * F.tile * F.tile * per_pixel;
+  // The persistent kernels claim items with 32-bit partition counters that overshoot the end by
+  // at most one refill per resident wave (< 2^20); frames with more items run path_kernel, whose
+  // item index is 64-bit (e.g. 8192^2 x 64 spp AA = 2^32 items).
+  P.persistent = persistent_supported(c->accel, c->gdim) && env_int("DRT_PERSISTENT", 1) != 0 &&
+                 F.n_items < kPersistentMaxItems;
   int slots = per_pixel;                                   // sample slots per pixel
   if (P.persistent && F.mode == MODE_SEQ) {  // a lane runs a pixel's samples in order, one slot each
     slots = c->spp ? (int)c->spp : (F.grid_res ? (int)F.grid_res : 1);
     F.nsub = slots;
   }
-  F.n_items = (uint64_t)F.n_my_tiles * F.tile * F.tile * per_pixel;
   P.n_slots = (uint64_t)F.n_my_tiles * F.tile * F.tile * slots;
   ReduceArgs& R = P.R;
   R.nsub = slots;
@@ -595,6 +610,20 @@ int drt_shard_layout(const drt_ctx* c, const drt_frame_params* p, int64_t* tiles
   const int64_t per_shard = (P.n_tiles + shards - 1) / shards;  // equal-size shard buffers
   if (tiles) *tiles = P.F.n_my_tiles;
   if (floats) *floats = per_shard * P.F.tile * P.F.tile * 3;
+  return DRT_OK;
+}
+
+int drt_plan_frame(const drt_ctx* c, const drt_frame_params* p, drt_frame_plan* out) {
+  if (!c || !p || !out) return DRT_E_INVALID;
+  Plan P;
+  int rc = plan_frame(const_cast<drt_ctx*>(c), p, P);
+  if (rc) return rc;
+  memset(out, 0, sizeof(*out));
+  out->work_items = P.F.n_items;
+  out->sample_slots = P.n_slots;
+  out->mode = P.F.mode;
+  out->persistent = P.persistent ? 1 : 0;
+  out->tiles_in_shard = P.F.n_my_tiles;
   return DRT_OK;
 }
 

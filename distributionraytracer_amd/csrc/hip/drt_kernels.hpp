@@ -47,6 +47,8 @@ constexpr int kRowShift = kPBlock == 256 ? 10 : (kPBlock == 128 ? 9 : 8);
 static_assert(kPBlock == 256 || kPBlock == 128 || kPBlock == 64, "persistent block: 64, 128 or 256 threads");
 constexpr size_t kMacroBits = 131072;  // Grid macro-cell bitmap budget: 16 KB of LDS per block
 constexpr size_t kPrimPadBytes = 64;  // zeroed tail of the primitive buffer (node_step's slot reads)
+// persistent kernels: 32-bit work-item counters; bigger frames run the 64-bit path_kernel
+constexpr uint64_t kPersistentMaxItems = 0xF0000000ull;
 
 struct SceneArgs {
   // Camera (camera.h:32-61), precomputed on the host

@@ -172,6 +172,20 @@ int drt_upload_bvh(drt_ctx* ctx, const drt_bvh_node* nodes, uint32_t n_nodes, co
 int drt_upload_grid(drt_ctx* ctx, const int32_t dims[3], const float bmin[3], const float bmax[3],
                     const int64_t* cell_start /* nx*ny*nz+1 */, const int32_t* cell_objs, int64_t n_refs);
 
+/* How a frame would run (no device work): work items (a (pixel, sample) pair, or a pixel whose
+ * samples run in order), float4 sample slots, the frame mode (0 AA, 1 in-order keyed stream,
+ * 2 Whitted quad grid, 3 Whitted point, 4 progressive) and whether the persistent kernel takes it
+ * (frames of >= 0xF0000000 work items run the 64-bit one-item-per-thread kernel instead). */
+typedef struct {
+  uint64_t work_items;
+  uint64_t sample_slots;
+  int32_t mode;
+  int32_t persistent;
+  int32_t tiles_in_shard;
+  int32_t reserved[5];
+} drt_frame_plan;
+int drt_plan_frame(const drt_ctx* ctx, const drt_frame_params* params, drt_frame_plan* out);
+
 /* Whole frame into host memory (RES_Y*RES_X*3 floats). */
 int drt_render(drt_ctx* ctx, const drt_frame_params* params, float* rgb_out);
 

@@ -292,15 +292,20 @@ def test_streaming_traverse_many_chunks_matches_oracle(drt, oracle_mod, renderer
     np.testing.assert_array_equal(renderer.trace_shadow(rays), b.trace_shadow(rays))
 
 
-# BASELINE.json configs at their full sizes: the GPU renders the whole frame, the oracle a band
-# of rows of the same frame (its cost is per row; the keyed RNG makes rows independent).
+# BASELINE.json configs at their full sizes: the GPU renders the whole frame, the oracle a set of
+# rows spread over the same frame — top (sky), middle (objects, glass, mirrors), bottom (floor)
+# and both edge rows (its cost is per row; the keyed RNG makes rows independent).
+def spread_rows(res, n):
+    return sorted(set(np.linspace(0, res - 1, n).round().astype(int).tolist()))
+
+
 FULL_SIZE = {
     # name: (scene, render kwargs, oracle rows (None = the whole frame))
     "C2_balls_low_bvh_512_16spp": (dict(scene="balls_low", res=512, spp=16), {}, None),
-    "C3_tri100k_512_64spp_soft4": (dict(tris=100_000, res=512, spp=64), {"light_spp": 4}, (300, 304)),
-    "headline_tri1M_512_64spp": (dict(tris=1_000_000, res=512, spp=64), {}, (250, 254)),
+    "C3_tri100k_512_64spp_soft4": (dict(tris=100_000, res=512, spp=64), {"light_spp": 4}, spread_rows(512, 32)),
+    "headline_tri1M_512_64spp": (dict(tris=1_000_000, res=512, spp=64), {}, spread_rows(512, 32)),
     "C4_tri1M_1024_64spp_dof_glossy_depth8": (dict(tris=1_000_000, res=1024, spp=64, aperture=8.0, focal=1.0),
-                                              {"roughness": 0.1, "max_depth": 8}, (600, 602)),
+                                              {"roughness": 0.1, "max_depth": 8}, spread_rows(1024, 20)),
 }
 
 
@@ -320,11 +325,17 @@ def test_full_size_config_matches_oracle(drt, oracle_mod, renderer, case):
     img = renderer.render(seed=7, **kw)
     b = bench.make_scene(oracle_mod, args, tris, ext)
     b.build()
-    ref, _ = b.render(seed=7, rows=rows, **kw)
-    y0, y1 = rows if rows else (0, sk["res"])
-    compare_images(img[y0:y1], ref[y0:y1])
-    if rows:  # rows outside the band: rendered, finite, clamped
-        assert np.isfinite(img).all() and img.min() >= 0.0 and img.max() <= 1.0
+    if rows is None:
+        ref, _ = b.render(seed=7, **kw)
+        compare_images(img, ref)
+        return
+    for y in rows:
+        ref, _ = b.render(seed=7, rows=(y, y + 1), **kw)
+        compare_images(img[y:y + 1], ref[y:y + 1])
+    # rows outside the checked set: rendered, finite, clamped
+    assert np.isfinite(img).all() and img.min() >= 0.0 and img.max() <= 1.0
+    # the checked rows cover sky, objects and floor: not all one colour
+    assert len({tuple(np.round(img[y].mean(axis=0), 3)) for y in rows}) > len(rows) // 2
 
 
 @pytest.mark.parametrize("accel,spp", [("bvh", 4), ("grid", 0), ("none", 4)])
@@ -410,3 +421,59 @@ def test_shuffle_prepass_matches_in_kernel_walk(drt, renderer, tmp_path, apertur
     walk = renderer.render(seed=5)
     np.testing.assert_array_equal(with_perm.view(np.uint32), walk.view(np.uint32))
 
+
+
+def test_failed_upload_leaves_no_scene(drt, renderer, tmp_path):
+    """drt_upload_scene validates the whole descriptor before it commits anything: after a
+    rejected upload (bad primitive type, malformed skybox face, bad light type) the context has
+    no scene, so a render returns DRT_E_STATE instead of reading the old buffers."""
+    import ctypes as C
+
+    from distributionraytracer_amd import _lib
+
+    L = _lib.load()
+    p = sg.write(tmp_path, "s.p3f", sg.mixed_scene_text(res=(24, 16), spp=1, accel="bvh", n_tris=20))
+    good = drt.Scene.load_p3f(p)
+    cam = good.camera_frame()
+    cam.res_x, cam.res_y = 640, 480  # a bigger frame than the scene that is resident
+    mat = (_lib.DrtMaterial * 1)()
+    prim = (_lib.DrtPrim * 1)()
+    light = (_lib.DrtLight * 1)()
+    prim[0].type, prim[0].material, prim[0].r = 1, 0, 0.5
+    variants = {"bad prim type": lambda d: setattr(prim[0], "type", 7),
+                "bad light type": lambda d: setattr(light[0], "type", 5),
+                "skybox face missing": lambda d: setattr(d, "has_skybox", 1)}
+    for what, spoil in variants.items():
+        renderer.upload(good)
+        renderer.render(seed=1)
+        prim[0].type, light[0].type = 1, 0
+        d = _lib.DrtSceneDesc()
+        d.camera = cam
+        d.materials, d.n_materials = mat, 1
+        d.prims, d.n_prims = prim, 1
+        d.lights, d.n_lights = light, 1
+        d.accel, d.spp = 2, 1
+        spoil(d)
+        rc = L.drt_upload_scene(renderer.h, C.byref(d))
+        assert rc == -1, (what, rc)
+        out = np.zeros((480, 640, 3), np.float32)
+        params = renderer.frame_params(seed=1)
+        assert L.drt_render(renderer.h, C.byref(params), out.ctypes.data_as(_lib._f)) == -5, what
+        assert not out.any()
+    renderer.upload(good)  # a good upload restores the context
+
+
+def test_frame_plan_routes_huge_frames_to_64bit_kernel(drt, renderer, tmp_path):
+    """8192^2 x 64 spp AA is exactly 2^32 work items: the persistent kernel's 32-bit claim
+    counters would wrap, so the plan hands the frame to the 64-bit path_kernel."""
+    text = sg.mixed_scene_text(res=(8192, 8192), spp=64, accel="bvh", n_tris=20)
+    renderer.upload(drt.Scene.load_p3f(sg.write(tmp_path, "big.p3f", text)))
+    plan = renderer.plan(renderer.frame_params(seed=1))
+    assert plan["work_items"] == 2 ** 32 and plan["sample_slots"] == 2 ** 32 and plan["mode"] == 0
+    assert not plan["persistent"]
+    small = sg.mixed_scene_text(res=(512, 512), spp=64, accel="bvh", n_tris=20)
+    renderer.upload(drt.Scene.load_p3f(sg.write(tmp_path, "small.p3f", small)))
+    plan = renderer.plan(renderer.frame_params(seed=1))
+    assert plan["work_items"] == 512 * 512 * 64 and plan["persistent"]
+    plan = renderer.plan(renderer.frame_params(seed=1, roughness=0.1))  # in-order keyed stream
+    assert plan["mode"] == 1 and plan["work_items"] == 512 * 512 and plan["sample_slots"] == 512 * 512 * 64

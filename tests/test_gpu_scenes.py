@@ -1,0 +1,94 @@
+"""GPU parity on the reference's shipped scenes (P3D_Scenes/*.p3f, from the data fixture
+tests/golden/shipped_scenes.npz) and on BASELINE config C1.
+
+Each scene is loaded by the product's P3F loader and by the oracle's from the same text, with
+the same (downsampled) skybox faces, rendered on the HIP path and by the oracle with the same
+keyed-RNG seed, and compared per channel within TOL; traversal counts must be identical.
+Resolutions are the shipped ones (the oracle finishes each in seconds) except where a case
+overrides them.
+"""
+import numpy as np
+import pytest
+
+from tests import shipped
+from tests.test_gpu_parity import TOL, compare_images
+
+pytestmark = pytest.mark.gpu
+
+# name: (P3F overrides, render kwargs)
+SCENE_CASES = {
+    # BASELINE.json configs[0] (C1): balls_low, accel none, 256x256, 1 spp — whole frame
+    "C1_balls_low_none_256_1spp": ("balls_low", dict(res=(256, 256), spp=1), {}),
+    "balls_low_shipped_none_16spp": ("balls_low", {}, {}),
+    "balls_low_grid_16spp": ("balls_low", dict(accel="grid"), {}),
+    "balls_low_bvh_16spp_C2": ("balls_low", dict(accel="bvh"), {}),
+    "dof_none_aperture12": ("dof", {}, {}),
+    "dof_bvh_aperture12": ("dof", dict(accel="bvh"), {}),
+    "motion_none_spp32_n5": ("motion", {}, {}),
+    "teste_none_16spp": ("teste", {}, {}),
+    "teste_grid_16spp": ("teste", dict(accel="grid"), {}),
+    "balls_box_grid_whitted_sky": ("balls_box", {}, {}),
+    "balls_high_grid_whitted_sky": ("balls_high", {}, {}),
+    "balls_high_bvh_whitted_sky": ("balls_high", dict(accel="bvh"), {}),
+    "blueDiamond_grid_glass_sky": ("blueDiamond", {}, {}),
+    "dragon_grid_whitted_sky": ("dragon", {}, {}),
+    "assignment1_grid_whitted_sky": ("assignment1", {}, {}),
+    "dragon_assignment1_bvh_whitted_sky": ("dragon_assignment1", {}, {}),
+    "dragon_assignment1_bvh_aa16": ("dragon_assignment1", dict(res=(256, 256), spp=16), {}),
+}
+
+
+@pytest.fixture(scope="module")
+def drt():
+    import distributionraytracer_amd as d
+
+    return d
+
+
+@pytest.fixture(scope="module")
+def renderer(drt):
+    r = drt.Renderer(0)
+    yield r
+    r.close()
+
+
+def load_both(drt, O, tmp_path, name, **over):
+    p = shipped.write(tmp_path, name, **over)
+    faces = shipped.skybox_faces(name)
+    return drt.Scene.load_p3f(p, skybox_faces=faces), O.Scene.load_p3f(p, skybox_faces=faces)
+
+
+@pytest.mark.parametrize("case", sorted(SCENE_CASES))
+def test_shipped_scene_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
+    name, over, kw = SCENE_CASES[case]
+    a, b = load_both(drt, oracle_mod, tmp_path, name, **over)
+    renderer.upload(a)
+    img = renderer.render(seed=2718, stats=True, **kw)
+    st = renderer.stats()
+    ref, rst = b.render(seed=2718, **kw)
+    exact = compare_images(img, ref, TOL)
+    assert exact > 0.5, f"only {exact:.3f} of the channels are bit-identical"
+    acc = a.info().accel
+    if acc != 0:
+        assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
+    if acc == 2:
+        for k in ("closest_inner", "closest_leaf", "shadow_inner", "shadow_leaf", "closest_prims", "shadow_prims"):
+            assert st[k] == rst[k], k
+    assert st["samples"] == rst["samples"]
+    if shipped.env(name):  # the sky, not bclr, fills the misses
+        assert a.info().skybox_loaded
+
+
+def test_dragon_assignment1_traversal_count_matches_reference_run(drt, renderer, tmp_path):
+    """the reference renders dragon_assignment1 (Whitted, BVH, 512x512) with
+    1 436 437 BVH::Traverse calls (closest + shadow).  RNG-independent: it pins the BVH, the
+    primitive intersection and rayTracing's branching end to end — here on the HIP path."""
+    p = shipped.write(tmp_path, "dragon_assignment1")
+    s = drt.Scene.load_p3f(p, skybox_faces=shipped.skybox_faces("dragon_assignment1"))
+    renderer.upload(s)
+    img = renderer.render(seed=1, stats=True)
+    st = renderer.stats()
+    assert img.shape == (512, 512, 3)
+    assert st["closest_rays"] + st["shadow_rays"] == 1436437
+    # Whitted: one sample per pixel (light 0 is punctual)
+    assert st["samples"] == 512 * 512

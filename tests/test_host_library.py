@@ -181,3 +181,32 @@ def test_write_png_is_upright_rgb8(tmp_path):
     assert img.shape == (6, 11, 3) and img.dtype == np.uint8
     # lower-left-origin frame: the PNG's top row is the frame's last row (DevIL, main.cpp:251-266)
     np.testing.assert_array_equal(img, _u8fromfloat(f)[::-1])
+
+
+@pytest.mark.parametrize("scene", ["balls_low", "dof", "motion", "teste", "balls_box", "balls_high", "blueDiamond",
+                                   "dragon", "assignment1", "dragon_assignment1"])
+def test_shipped_scene_fixture_loads_like_oracle(oracle_mod, tmp_path, scene):
+    """Every shipped scene (data fixture, no reference checkout needed): the product's loader
+    and the oracle's parse the same objects, lights, camera and accelerator, and the product's
+    parallel BVH build gives the oracle's tree."""
+    from tests import shipped
+
+    p = shipped.write(tmp_path, scene)
+    faces = shipped.skybox_faces(scene)
+    a = drt.Scene.load_p3f(p, skybox_faces=faces)
+    b = oracle_mod.Scene.load_p3f(p, skybox_faces=faces)
+    ia, ib = a.info(), b.info()
+    for k in ("res_x", "res_y", "spp", "accel", "n_objects", "n_lights", "n_materials", "has_env"):
+        assert getattr(ia, k) == getattr(ib, k), k
+    assert ia.skybox_loaded == (faces is not None)
+    fa = a.camera_frame()
+    mine = np.array([fa.plane_dist, fa.aperture, fa.w, fa.h, *fa.u, *fa.v, *fa.n], np.float32)
+    np.testing.assert_array_equal(bits(mine), bits(b.camera_frame()))
+    a.set_accel("bvh")
+    b.set_accel("bvh")
+    a.build()
+    b.build()
+    x, y = a.bvh_export(), b.bvh_export()
+    for k in ("leaf", "index", "nobjs", "order"):
+        np.testing.assert_array_equal(x[k], y[k], err_msg=k)
+    np.testing.assert_array_equal(bits(x["boxes"]), bits(y["boxes"]))

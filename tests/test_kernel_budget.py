@@ -1,0 +1,67 @@
+"""Register budget of the hot kernels (CPU test: reads the compiler's resource remarks).
+
+The persistent BVH kernel's loop sits on a register-allocation edge: DESIGN.md §4 records
+unrelated edits moving it by -6 % to -85 % when the allocator changed the VGPR count, spilled
+or dropped a wave per SIMD.  The build writes hipcc's `-Rpass-analysis=kernel-resource-usage`
+remarks next to each object (distributionraytracer_amd/csrc/build/*.remarks); this test fails
+when a hot instantiation leaves its budget, so such an edit fails a test, not a bench.
+"""
+import re
+import subprocess
+
+import pytest
+
+from distributionraytracer_amd import _lib
+
+REMARKS = _lib.CSRC / "build" / "drt_kernels.remarks"
+
+# demangled-name prefix: (max VGPRs, max scratch bytes per lane, min waves per SIMD, max VGPR
+# spills).  The scratch figure holds the private frame stack and the traversal stack's overflow
+# part as well as the spill slots; the spills counted here are the allocator's, and the loop is
+# tuned around the current ones (mostly shading state parked across the node loop).
+BUDGET = {
+    # headline (BASELINE configs[1..3]): AA frames, triangle-only scene, no stats
+    "drt::path_persistent<true, false, 0, 6, 2>": (80, 2336, 6, 69),
+    # C4: in-order keyed-stream frames (DoF / glossy)
+    "drt::path_persistent<true, false, 1, 6, 2>": (80, 2432, 6, 130),
+    # Whitted point-light frames on mixed primitives (the shipped Whitted scenes on a BVH)
+    "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 68),
+    # Grid stepper, AA frames
+    "drt::path_persistent<true, false, 0, 6, 1>": (80, 1840, 6, 191),
+}
+
+
+def parse_remarks(text):
+    out, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][A-Za-z /\[\]]*?): (\d+) \[", line)
+        if m and cur:
+            out[cur][m.group(1).strip()] = int(m.group(2))
+    return out
+
+
+@pytest.fixture(scope="module")
+def resources():
+    if not REMARKS.exists():
+        _lib.build()
+    kernels = parse_remarks(REMARKS.read_text())
+    names = list(kernels)
+    dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True, check=True)
+    return {d.removeprefix("void "): kernels[n] for n, d in zip(names, dem.stdout.splitlines())}
+
+
+@pytest.mark.parametrize("prefix", sorted(BUDGET))
+def test_hot_kernel_stays_in_register_budget(resources, prefix):
+    max_vgpr, max_scratch, min_waves, max_spill = BUDGET[prefix]
+    hits = [r for d, r in resources.items() if d.startswith(prefix + "(")]
+    assert len(hits) == 1, f"{prefix}: {len(hits)} instantiations in the remarks"
+    r = hits[0]
+    assert r["VGPRs"] <= max_vgpr, f"{prefix}: {r['VGPRs']} VGPRs > {max_vgpr}"
+    assert r["ScratchSize [bytes/lane]"] <= max_scratch, f"{prefix}: scratch {r['ScratchSize [bytes/lane]']} B"
+    assert r["Occupancy [waves/SIMD]"] >= min_waves, f"{prefix}: {r['Occupancy [waves/SIMD]']} waves/SIMD"
+    assert r["VGPRs Spill"] <= max_spill, f"{prefix}: {r['VGPRs Spill']} VGPR spills > {max_spill}"

@@ -133,24 +133,41 @@ def test_rng_draw_order_identical_to_reference(oracle_mod, sphere):
     np.testing.assert_array_equal(bits(vals), bits(g[f"rnd{sphere}_vals"]))
 
 
-@needs_reference
-def test_dragon_assignment1_traversal_count_matches_reference_run(oracle_mod):
+def test_dragon_assignment1_traversal_count_matches_reference_run(oracle_mod, tmp_path):
     """the reference renders dragon_assignment1 (Whitted, BVH, 512x512) with
     1 436 437 BVH::Traverse calls (closest + shadow).  RNG-independent, so it pins primitive
-    intersection, the BVH and the rayTracing recursion/branching end to end."""
+    intersection, the BVH and the rayTracing recursion/branching end to end.  The scene comes
+    from the shipped-scenes data fixture (tests/golden/shipped_scenes.npz)."""
+    from tests import shipped
+
     O = oracle_mod
-    s = O.Scene.load_p3f(SCENES / "dragon_assignment1.p3f", skybox_max_size=64)
+    s = O.Scene.load_p3f(shipped.write(tmp_path, "dragon_assignment1"),
+                         skybox_faces=shipped.skybox_faces("dragon_assignment1"))
     s.build()
     img, st = s.render(seed=1)
     assert st["closest_calls"] + st["shadow_calls"] == 1436437
     assert np.isfinite(img).all()
 
 
-@needs_reference
-def test_dragon_grid_cell_count_matches_reference_run(oracle_mod):
+def test_dragon_grid_cell_count_matches_reference_run(oracle_mod, tmp_path):
     """dragon.p3f builds a uniform grid of 814 318 cells."""
+    from tests import shipped
+
     O = oracle_mod
-    s = O.Scene.load_p3f(SCENES / "dragon.p3f", skybox_max_size=16)
+    s = O.Scene.load_p3f(shipped.write(tmp_path, "dragon"), skybox_faces=shipped.skybox_faces("dragon"))
     s.build()
     d = s.grid_export()["dims"]
     assert d[0] * d[1] * d[2] == 814318
+
+
+@needs_reference
+def test_shipped_scene_fixture_is_byte_identical_to_reference():
+    """tests/golden/shipped_scenes.npz rebuilds every shipped P3F file byte for byte."""
+    import hashlib
+
+    from tests import shipped
+
+    for name in shipped.names():
+        raw = (SCENES / f"{name}.p3f").read_bytes()
+        assert shipped.text(name) == raw, name
+        assert hashlib.sha1(raw).hexdigest().encode() == shipped._npz()[f"{name}/sha1"].tobytes()
