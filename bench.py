@@ -33,6 +33,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+# the vector-memory ceiling of the path kernel's access shape (dependent 64-B per-lane record
+# gathers at 6 waves/SIMD), measured by tools/gather_ceiling.hip on one MI355X
+CEILING_JSON = ROOT / "profiles" / "gather_ceiling.json"
 NODE_BYTES, PRIM_BYTES = 64, 48  # one inner-node record (both child boxes), one primitive record
 CAMERA = dict(eye=(2.1, 1.3, 1.7), at=(0.0, 0.0, 0.0), up=(0.0, 0.0, 1.0), fovy=45.0, hither=0.01)
 FLOOR = np.array([[-4, -4, -1.2, 4, -4, -1.2, 4, 4, -1.2], [-4, -4, -1.2, 4, 4, -1.2, -4, 4, -1.2]], np.float32)
@@ -104,6 +107,31 @@ def cpu_baseline(args, tris, res, spp, seed, target_s, threads, ext):
             "sample": f"rows {y0}-{y0 + rows - 1} of the {res}x{res}x{spp}spp frame ({rows * res * spp} samples, "
                       f"{rays} rays) in {dt:.1f} s; oracle BVH build {build_s:.1f} s",
             "seconds": round(dt, 2)}
+
+
+def interval_union(starts, ends):
+    """Total length of the union of [start, end) intervals."""
+    tot, cur_s, cur_e = 0.0, None, None
+    for a, b in sorted(zip(starts, ends)):
+        if cur_e is None or a > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
+
+
+def load_ceiling():
+    """The measured gather ceiling (profiles/gather_ceiling.json): the fastest table's rate."""
+    try:
+        c = json.loads(CEILING_JSON.read_text())
+        return {"peak_GB_per_s": c["peak_GB_per_s"], "table_bytes": c["peak_table_bytes"],
+                "source": "profiles/gather_ceiling.json (tools/gather_ceiling.hip)"}
+    except Exception:
+        return None
 
 
 def main():
@@ -240,10 +268,18 @@ def main():
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
+    # roofline.kernel_ms: device time the path kernel held per step over the timed region — the
+    # union of the timed frames' path-kernel spans (HIP events on each frame's stream, one device
+    # clock) divided by the steps.  Frames in flight overlap, so a single frame's span also holds
+    # its wait for the other frame's blocks; the union counts every instant once.
+    try:
+        ps, pe, _ = r.frame_spans(args.steps)
+        kernel_ms = interval_union(ps, pe) / max(1, len(ps))
+    except AttributeError:  # an A/B build (DRT_LIBRARY) older than drt_frame_spans
+        kernel_ms = None
 
-    # roofline.kernel_ms: the path kernel's own duration per launch.  Frames in flight overlap, so
-    # a pipelined frame's HIP-event span also holds its wait for the other frame's blocks; time a
-    # few frames one at a time on one stream instead (untimed, after the timed region).
+    # the path kernel of frames rendered one at a time (untimed, after the timed region): its
+    # launch duration alone, for the rocprof per-dispatch average
     serial = 3
     for _ in range(serial):
         r.render_device(shard_p, (frames[0] if world == 1 else fgs[0].shard).data_ptr(), sptr)
@@ -267,10 +303,13 @@ def main():
         t_h = time.perf_counter()
         r.render(seed=args.seed, **fkw)
         host_frame_ms = (time.perf_counter() - t_h) * 1e3
-    kernel_ms = float(np.mean(path_ms)) if len(path_ms) else float("nan")
+    serial_ms = float(np.mean(path_ms)) if len(path_ms) else float("nan")
+    if kernel_ms is None:
+        kernel_ms = serial_ms
     bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    ceiling = load_ceiling()
     traffic = None
     dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh", "ks": 0.5}
     extras = [f"{k}{v if isinstance(v, str) else format(v, 'g')}" for k, v in ext.items() if v != dflt[k]]
@@ -310,10 +349,18 @@ def main():
                    "scene": args.scene, "tris": args.tris if args.scene == "synthetic" else 0, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
                    "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
                    "frames_in_flight": pipe},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        # bound: the per-CU vector-memory path serving dependent 64-B per-lane record gathers (TA/TD
+        # busy 98 %), peak = tools/gather_ceiling.hip's fastest table; achieved =
+        # algorithmic record bytes (64 B per inner-node visit + 48 B per primitive test) per second
+        # of path-kernel device time.  hbm_frac: PMC-measured fabric bytes per launch against 8 TB/s.
+        "roofline": {"bound": "vmem_gather", "achieved": round(achieved, 1),
+                     "peak": ceiling["peak_GB_per_s"] if ceiling else None, "unit": "GB/s",
+                     "frac": round(achieved / ceiling["peak_GB_per_s"], 4) if ceiling else None,
+                     "traffic": traffic,
+                     "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                      "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),
-                     "kernel_ms": round(kernel_ms, 3)},
+                     "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),
+                     "ceiling": ceiling},
         "host_output_frame_ms": None if host_frame_ms is None else round(host_frame_ms, 3),
         **({"frame_check_vs_whole_frame": frame_check} if args.check_frame else {}),
         "rays_per_frame": int(rays_frame),

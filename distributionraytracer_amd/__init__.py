@@ -290,6 +290,15 @@ class Renderer:
             check(n, self.h, "drt_frame_times")
         return np.array(a[:n]), np.array(b[:n])
 
+    def frame_spans(self, max_frames=512):
+        """(path start, path end, frame end) of recent frames in ms on one device clock, from the
+        oldest frame's path-kernel start (HIP events on each frame's stream)."""
+        a, b, e = ((C.c_double * max_frames)() for _ in range(3))
+        n = _lib.load().drt_frame_spans(self.h, max_frames, a, b, e)
+        if n < 0:
+            check(n, self.h, "drt_frame_spans")
+        return np.array(a[:n]), np.array(b[:n]), np.array(e[:n])
+
     def trace_closest(self, rays):
         r = _f32(rays).reshape(-1, 6)
         n = len(r)

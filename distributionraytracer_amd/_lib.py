@@ -115,6 +115,8 @@ SIGNATURES = {
     "drt_trace_stats": (C.c_int, [_vp, C.POINTER(DrtFrameStats)]),
     "drt_get_stats": (C.c_int, [_vp, C.POINTER(DrtFrameStats)]),
     "drt_frame_times": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "drt_frame_spans": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_double)]),
     # drt_host.h
     "drt_scene_new": (_vp, []),
     "drt_scene_load_p3f": (_vp, [C.c_char_p]),

@@ -681,6 +681,28 @@ int drt_frame_times(drt_ctx* c, int max_frames, double* path_ms, double* total_m
   return n;
 }
 
+int drt_frame_spans(drt_ctx* c, int max_frames, double* path_start, double* path_end, double* frame_end) {
+  if (!c || max_frames < 0) return DRT_E_INVALID;
+  const uint64_t have = std::min<uint64_t>(c->frames, (uint64_t)drt_ctx::kRing);
+  const int n = (int)std::min<uint64_t>(have, (uint64_t)max_frames);
+  if (n == 0) return 0;
+  DRT_HIP(c, hipSetDevice(c->device));
+  const uint64_t f0 = c->frames - (uint64_t)n;
+  hipEvent_t base = c->ring[3 * (f0 % drt_ctx::kRing)];
+  for (int i = 0; i < n; i++) {
+    hipEvent_t* ev = &c->ring[3 * ((f0 + (uint64_t)i) % drt_ctx::kRing)];
+    DRT_HIP(c, hipEventSynchronize(ev[2]));
+    float a = 0, b = 0, e = 0;
+    DRT_HIP(c, hipEventElapsedTime(&a, base, ev[0]));
+    DRT_HIP(c, hipEventElapsedTime(&b, base, ev[1]));
+    DRT_HIP(c, hipEventElapsedTime(&e, base, ev[2]));
+    if (path_start) path_start[i] = a;
+    if (path_end) path_end[i] = b;
+    if (frame_end) frame_end[i] = e;
+  }
+  return n;
+}
+
 int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
   if (!c || !out) return DRT_E_INVALID;
   memset(&c->last, 0, sizeof(c->last));

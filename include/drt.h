@@ -227,6 +227,10 @@ int drt_get_stats(drt_ctx* ctx, drt_frame_stats* out);
  * path-tracing kernel (path_ms) and kernel + reduce (total_ms), from HIP events recorded on the
  * stream each frame ran on.  Waits for those frames.  Returns the count written (>= 0). */
 int drt_frame_times(drt_ctx* ctx, int max_frames, double* path_ms, double* total_ms);
+/* The same frames as absolute spans on one device clock, in ms from the path-kernel start of the
+ * oldest frame returned: path-kernel start / end and frame end.  Frames on different streams
+ * overlap; the union of their path-kernel spans is the device time the path kernel held. */
+int drt_frame_spans(drt_ctx* ctx, int max_frames, double* path_start, double* path_end, double* frame_end);
 
 #ifdef __cplusplus
 }

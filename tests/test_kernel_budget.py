@@ -21,13 +21,13 @@ REMARKS = _lib.CSRC / "build" / "drt_kernels.remarks"
 # tuned around the current ones (mostly shading state parked across the node loop).
 BUDGET = {
     # headline (BASELINE configs[1..3]): AA frames, triangle-only scene, no stats
-    "drt::path_persistent<true, false, 0, 6, 2>": (80, 2336, 6, 69),
+    "drt::path_persistent<true, false, 0, 6, 2>": (80, 2336, 6, 67),
     # C4: in-order keyed-stream frames (DoF / glossy)
-    "drt::path_persistent<true, false, 1, 6, 2>": (80, 2432, 6, 130),
+    "drt::path_persistent<true, false, 1, 6, 2>": (80, 2416, 6, 106),
     # Whitted point-light frames on mixed primitives (the shipped Whitted scenes on a BVH)
-    "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 68),
+    "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 65),
     # Grid stepper, AA frames
-    "drt::path_persistent<true, false, 0, 6, 1>": (80, 1840, 6, 191),
+    "drt::path_persistent<true, false, 0, 6, 1>": (80, 1852, 6, 245),
 }
 
 

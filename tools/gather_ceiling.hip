@@ -1,0 +1,122 @@
+// gather_ceiling.hip — the vector-memory ceiling for the BVH kernel's access shape on one MI355X.
+//
+// The persistent path kernel's node step is a per-lane gather: every traversing lane loads one
+// 64-B record (4 x 16-B slots, global_load_dwordx4) whose address depends on the previous
+// record, with one record in flight per lane, at 6 waves per SIMD.  This program
+// runs exactly that shape with nothing else — a dependent chain of random 64-B records per lane —
+// over tables of several sizes (L1-, L2-, Infinity-Cache- and HBM-resident), and reports the
+// record bytes served per second.  The fastest table is the ceiling the path kernel cannot
+// exceed however much locality its rays have; bench.py's roofline.frac divides the kernel's
+// algorithmic record bytes per second by it (roofline.bound "vmem_gather").
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/gather_ceiling tools/gather_ceiling.hip
+//   tools/bin/gather_ceiling [chains]      -> one JSON line per table size
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                        \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                          \
+    }                                                                                   \
+  } while (0)
+
+constexpr int kBlock = 256;
+constexpr int kWaves = 6;  // waves per SIMD, the path kernel's occupancy
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// CHAINS independent dependent chains per lane (1 = the node step: one record in flight).
+template <int CHAINS>
+__global__ void __launch_bounds__(kBlock, kWaves) gather(const float4* __restrict__ table, uint32_t mask,
+                                                          uint32_t iters, float* __restrict__ out) {
+  const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t idx[CHAINS];
+  for (int c = 0; c < CHAINS; c++) idx[c] = mix(tid * 0x9E3779B9u + c) & mask;
+  float acc = 0.0f;
+  for (uint32_t it = 0; it < iters; it++) {
+    for (int c = 0; c < CHAINS; c++) {
+      const float4* r = table + 4 * (size_t)idx[c];
+      const float4 a = r[0], b = r[1], d = r[2], e = r[3];
+      acc += a.y + b.x + b.w + d.z + e.w;
+      // the next record depends on this one (a BVH child descriptor does the same)
+      idx[c] = mix(idx[c] ^ __float_as_uint(a.x) ^ __float_as_uint(e.x)) & mask;
+    }
+  }
+  out[tid] = acc;
+}
+
+// Dynamic LDS per block (unused) that caps the CU at kWaves blocks of 256 threads, i.e. kWaves
+// waves per SIMD: the gather kernel's few registers would otherwise let 8 in.
+constexpr size_t kLdsPad = 160 * 1024 / kWaves - 1024;
+
+template <int CHAINS>
+static double run(const float4* d_table, uint32_t n_rec, uint32_t iters, int blocks, float* d_out) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  gather<CHAINS><<<blocks, kBlock, kLdsPad>>>(d_table, n_rec - 1, 4, d_out);  // warm caches / code
+  CHECK(hipGetLastError());
+  CHECK(hipEventRecord(a));
+  gather<CHAINS><<<blocks, kBlock, kLdsPad>>>(d_table, n_rec - 1, iters, d_out);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms;
+}
+
+int main(int argc, char** argv) {
+  const int chains = argc > 1 ? atoi(argv[1]) : 1;
+  hipDeviceProp_t prop;
+  CHECK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  int per_cu = 0;
+  if (chains == 1)
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gather<1>, kBlock, kLdsPad));
+  else
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gather<2>, kBlock, kLdsPad));
+  const int blocks = cus * per_cu;
+  // table sizes in 64-B records (powers of two): 16 KiB (L1), 2 MiB (L2), 128 MiB (the 1M-triangle
+  // scene is 124 MB: Infinity Cache), 1 GiB (HBM)
+  const uint32_t sizes[] = {1u << 8, 1u << 15, 1u << 21, 1u << 24};
+  const uint32_t max_rec = 1u << 24;
+  std::vector<float> h(4 * 4 * (size_t)max_rec);
+  uint32_t s = 12345u;
+  for (auto& v : h) {
+    s = s * 1664525u + 1013904223u;
+    v = (float)(s >> 8) * (1.0f / 16777216.0f);
+  }
+  float4* d_table = nullptr;
+  float* d_out = nullptr;
+  CHECK(hipMalloc(&d_table, h.size() * sizeof(float)));
+  CHECK(hipMemcpy(d_table, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+  CHECK(hipMalloc(&d_out, (size_t)blocks * kBlock * sizeof(float)));
+  for (uint32_t n_rec : sizes) {
+    const uint32_t iters = n_rec <= (1u << 15) ? 3000 : 2000;
+    const double ms = chains == 1 ? run<1>(d_table, n_rec, iters, blocks, d_out) : run<2>(d_table, n_rec, iters, blocks, d_out);
+    const double recs = (double)blocks * kBlock * iters * chains;
+    printf("{\"table_bytes\": %llu, \"chains\": %d, \"blocks\": %d, \"waves_per_simd\": %d, \"ms\": %.3f, "
+           "\"records_per_s\": %.4e, \"GB_per_s\": %.1f}\n",
+           (unsigned long long)n_rec * 64ull, chains, blocks, per_cu * kBlock / 64 / 4, ms, recs / (ms * 1e-3),
+           recs * 64.0 / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+  }
+  CHECK(hipFree(d_table));
+  CHECK(hipFree(d_out));
+  return 0;
+}

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Path-kernel device time per step from a rocprofv3 kernel trace of `bench.py --steps K --warmup W`,
+computed the way bench.py computes roofline.kernel_ms from HIP events: the union of the timed
+dispatches' [start, end] spans divided by K.  Also the mean duration of the serial frames rendered
+after the timed region (roofline.kernel_ms_serial).
+
+Dispatch order of the non-stats path_persistent instantiation in bench.py: W warmup, K timed,
+3 serial, then (one GPU) 2 drt_render frames.
+
+usage: python tools/rocprof_union.py TRACE_DIR --steps K --warmup W
+"""
+import argparse
+import csv
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from bench import interval_union  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace_dir")
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--warmup", type=int, required=True)
+    a = ap.parse_args()
+    rows = []
+    for f in Path(a.trace_dir).rglob("*kernel_trace.csv"):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            if "path_persistent<" in k and k.split("<", 2)[1].split(",")[1].strip() == "false":
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
+    rows.sort()
+    timed = rows[a.warmup:a.warmup + a.steps]
+    serial = rows[a.warmup + a.steps:a.warmup + a.steps + 3]
+    union_ms = interval_union([s for s, _, _ in timed], [e for _, e, _ in timed]) / 1e6
+    res = {"kernel": timed[0][2] if timed else None, "dispatches": len(rows),
+           "kernel_ms_per_step_union": round(union_ms / max(1, len(timed)), 3),
+           "kernel_ms_serial_mean": round(sum(e - s for s, e, _ in serial) / max(1, len(serial)) / 1e6, 3),
+           "timed_span_ms": round((timed[-1][1] - timed[0][0]) / 1e6, 3) if timed else None}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
