@@ -92,6 +92,8 @@ class Scene:
         s = cls(h)
         env = s.env
         if env:
+            if skybox_faces is None and s.info().skybox_loaded:
+                return s  # Scene::load_p3f's LoadSkybox found the faces (PPM / registered decoder)
             if skybox_faces is None:
                 root = Path(skybox_root) if skybox_root else Path(path).resolve().parent.parent
                 skybox_faces = load_skybox_dir(root / env, skybox_max_size)
@@ -174,6 +176,35 @@ class Scene:
                                                index.ctypes.data_as(_lib._u32), nobj.ctypes.data_as(_lib._u32),
                                                order.ctypes.data_as(_lib._i32)), what="bvh_export")
         return dict(boxes=boxes, leaf=leaf, index=index, nobjs=nobj, order=order)
+
+    def trace_cpu(self, rays, shadow=False):
+        """The scalar host path (BVH::Traverse / Grid::Traverse / the NONE scan on the CPU, one ray
+        at a time): closest -> (t, normal, object); shadow -> occluded (uint8)."""
+        r = _f32(rays).reshape(-1, 6)
+        n = len(r)
+        L = _lib.load()
+        if shadow:
+            occ = np.zeros(n, np.uint8)
+            check(L.drt_scene_trace_cpu(self.h, 1, _fp(r), n, None, None, None, occ.ctypes.data_as(_lib._u8)),
+                  what="trace_cpu")
+            return occ
+        t = np.zeros(n, np.float32)
+        nrm = np.zeros((n, 3), np.float32)
+        obj = np.zeros(n, np.int32)
+        check(L.drt_scene_trace_cpu(self.h, 0, _fp(r), n, _fp(t), _fp(nrm), obj.ctypes.data_as(_lib._i32), None),
+              what="trace_cpu")
+        return t, nrm, obj
+
+    def skybox_color_cpu(self, dirs):
+        """Scene::GetSkyboxColor for n directions (n x 3 floats)."""
+        d = _f32(dirs).reshape(-1, 3)
+        out = np.zeros((len(d), 3), np.float32)
+        check(_lib.load().drt_scene_skybox_color_cpu(self.h, _fp(d), len(d), _fp(out)), what="skybox_color_cpu")
+        return out
+
+    def load_skybox(self, sky_dir):
+        """Scene::LoadSkybox: <dir>/<face>.ppm (or .jpg through a registered decoder)."""
+        check(_lib.load().drt_scene_load_skybox(self.h, str(sky_dir).encode()), what="load_skybox")
 
     def grid_export(self):
         L = _lib.load()

@@ -144,6 +144,10 @@ SIGNATURES = {
     "drt_scene_grid_export": (C.c_int, [_vp, _i64, _i32]),
     "drt_scene_camera_frame": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
     "drt_scene_upload": (C.c_int, [_vp, _vp]),
+    "drt_set_image_decoder": (C.c_int, [_vp, _vp]),
+    "drt_scene_load_skybox": (C.c_int, [_vp, C.c_char_p]),
+    "drt_scene_trace_cpu": (C.c_int, [_vp, C.c_int, _f, C.c_int64, _f, _f, _i32, _u8]),
+    "drt_scene_skybox_color_cpu": (C.c_int, [_vp, _f, C.c_int64, _f]),
     "drt_image_rgb8": (C.c_int, [_vp, C.c_int32, C.c_int32, _vp]),
     "drt_image_write_png": (C.c_int, [C.c_char_p, _vp, C.c_int32, C.c_int32]),
 }

@@ -13,7 +13,7 @@
 #include <future>
 #include <thread>
 
-#include "drt_scene.hpp"
+#include "../../../include/drt_scene.hpp"
 
 namespace drt {
 
@@ -232,9 +232,11 @@ void Grid::Build(std::vector<Object*>& objs) {  // grid.cpp:30-97
   auto t0 = std::chrono::steady_clock::now();
   AABB gb(Vector(FLT_MAX, FLT_MAX, FLT_MAX), Vector(-FLT_MAX, -FLT_MAX, -FLT_MAX));
   std::vector<AABB> bx(objs.size());
+  const size_t base = objects.size();  // positions of these objects in the grid's list
   for (size_t i = 0; i < objs.size(); i++) {
     bx[i] = objs[i]->GetBoundingBox();
     gb.extend(bx[i]);
+    addObject(objs[i]);
   }
   gb.min.x = (float)((double)gb.min.x - kEps); gb.min.y = (float)((double)gb.min.y - kEps);
   gb.min.z = (float)((double)gb.min.z - kEps);
@@ -272,7 +274,7 @@ void Grid::Build(std::vector<Object*>& objs) {  // grid.cpp:30-97
     range(bx[i], r);
     for (int iz = r[2]; iz <= r[5]; iz++)
       for (int iy = r[1]; iy <= r[4]; iy++)
-        for (int ix = r[0]; ix <= r[3]; ix++) cell_objs[(size_t)fill[(size_t)(ix + nx * iy + nx * ny * iz)]++] = objs[i]->scene_index;
+        for (int ix = r[0]; ix <= r[3]; ix++) cell_objs[(size_t)fill[(size_t)(ix + nx * iy + nx * ny * iz)]++] = (int32_t)(base + i);
   }
   build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -280,34 +282,11 @@ void Grid::Build(std::vector<Object*>& objs) {  // grid.cpp:30-97
 int Grid::upload(drt_ctx* ctx) const {
   const int32_t dims[3] = {nx, ny, nz};
   const float mn[3] = {bbox.min.x, bbox.min.y, bbox.min.z}, mx[3] = {bbox.max.x, bbox.max.y, bbox.max.z};
-  return drt_upload_grid(ctx, dims, mn, mx, cell_start.data(), cell_objs.data(), (int64_t)cell_objs.size());
+  // the device indexes scene-order primitive records: list positions -> scene indices
+  std::vector<int32_t> scene_ids(cell_objs.size());
+  for (size_t i = 0; i < cell_objs.size(); i++) scene_ids[i] = objects[(size_t)cell_objs[i]]->scene_index;
+  return drt_upload_grid(ctx, dims, mn, mx, cell_start.data(), scene_ids.data(), (int64_t)scene_ids.size());
 }
-
-// ---------------------------------------------------------------- GPU-backed Traverse()
-static bool closest_one(drt_ctx* ctx, const Scene* sc, Ray& ray, Object** hit_obj, HitRecord& rec) {
-  float r[6] = {ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x, ray.direction.y, ray.direction.z};
-  float t, nn[3];
-  int32_t obj;
-  if (!ctx || drt_trace_closest(ctx, r, 1, &t, nn, &obj) != DRT_OK) return false;
-  rec = HitRecord();
-  if (obj < 0) return false;
-  rec.isHit = true;
-  rec.t = t;
-  rec.normal = Vector(nn[0], nn[1], nn[2]);
-  if (hit_obj && sc) *hit_obj = sc->getObject((unsigned)obj);
-  return true;
-}
-static bool shadow_one(drt_ctx* ctx, Ray& ray) {
-  float r[6] = {ray.origin.x, ray.origin.y, ray.origin.z, ray.direction.x, ray.direction.y, ray.direction.z};
-  uint8_t occ = 0;
-  if (!ctx || drt_trace_shadow(ctx, r, 1, &occ) != DRT_OK) return false;
-  ray.direction.normalize();  // Traverse(Ray&) normalises the caller's ray (bvh.cpp:322, grid.cpp:312)
-  return occ != 0;
-}
-bool BVH::Traverse(Ray& ray, Object** hit_obj, HitRecord& rec) { return closest_one(ctx_, scene_, ray, hit_obj, rec); }
-bool BVH::Traverse(Ray& ray) { return shadow_one(ctx_, ray); }
-bool Grid::Traverse(Ray& ray, Object** hit_obj, HitRecord& rec) { return closest_one(ctx_, scene_, ray, hit_obj, rec); }
-bool Grid::Traverse(Ray& ray) { return shadow_one(ctx_, ray); }
 
 int upload_scene(drt_ctx* ctx, const Scene& scene, const BVH* bvh, const Grid* grid) {
   drt_scene_desc d;

@@ -2,7 +2,7 @@
 #include <cstring>
 
 #include "../../../include/drt_host.h"
-#include "drt_scene.hpp"
+#include "../../../include/drt_scene.hpp"
 
 using namespace drt;
 
@@ -140,8 +140,13 @@ int drt_scene_add_light_quad(drt_scene* s, const float p[3], const float c[3], c
 int drt_scene_build(drt_scene* s) {  // main.cpp:1023-1049
   if (!s) return DRT_E_INVALID;
   std::vector<Object*> objs = s->scene.objectList();
-  if (s->scene.GetAccelStruct() == BVH_ACC) s->bvh.Build(objs);
-  else if (s->scene.GetAccelStruct() == GRID_ACC) s->grid.Build(objs);
+  if (s->scene.GetAccelStruct() == BVH_ACC) {
+    s->bvh = BVH();
+    s->bvh.Build(objs);
+  } else if (s->scene.GetAccelStruct() == GRID_ACC) {
+    s->grid = Grid();  // Grid::Build appends to the grid's object list (grid.cpp:45)
+    s->grid.Build(objs);
+  }
   s->built = true;
   return DRT_OK;
 }
@@ -193,10 +198,68 @@ int drt_scene_upload(drt_ctx* ctx, drt_scene* s) {
   if (!s->scene.GetCamera()) return DRT_E_STATE;
   if (s->scene.GetSkyBoxFlg() && !s->scene.SkyboxComplete()) return DRT_E_STATE;
   if (!s->built) drt_scene_build(s);
-  int rc = upload_scene(ctx, s->scene, &s->bvh, &s->grid);
-  if (rc) return rc;
-  s->bvh.bind(ctx, &s->scene);
-  s->grid.bind(ctx, &s->scene);
+  return upload_scene(ctx, s->scene, &s->bvh, &s->grid);
+}
+
+int drt_scene_load_skybox(drt_scene* s, const char* dir) {
+  if (!s || !dir) return DRT_E_INVALID;
+  if (!s->scene.LoadSkybox(dir)) return DRT_E_INVALID;
+  s->scene.SetSkyBoxFlg(true);
+  return DRT_OK;
+}
+
+int drt_scene_trace_cpu(const drt_scene* s, int shadow, const float* rays, int64_t n, float* t, float* normal,
+                        int32_t* object, uint8_t* occluded) {
+  if (!s || n < 0 || (n && !rays)) return DRT_E_INVALID;
+  if (shadow ? (n && !occluded) : (n && (!t || !normal || !object))) return DRT_E_INVALID;
+  if (!s->built) return DRT_E_STATE;
+  const Scene& sc = s->scene;
+  const accelerator acc = sc.GetAccelStruct();
+  for (int64_t i = 0; i < n; i++) {
+    const float* r = rays + 6 * i;
+    Ray ray(Vector(r[0], r[1], r[2]), Vector(r[3], r[4], r[5]));
+    if (shadow) {
+      bool occ = false;
+      if (acc == BVH_ACC) occ = s->bvh.Traverse(ray);
+      else if (acc == GRID_ACC) occ = s->grid.Traverse(ray);
+      else {  // the NONE loop of main.cpp:432-439 without its self-skip (a raw query has no hit
+              // object): a hit with t in (1e-4, |d|) along d occludes
+        const float len = ray.direction.length();
+        for (int k = 0; k < sc.getNumObjects() && !occ; k++) {
+          const HitRecord h = sc.getObject((unsigned)k)->hit(ray);
+          occ = h.isHit && h.t > 1e-4f && h.t < len;
+        }
+      }
+      occluded[i] = occ ? 1 : 0;
+      continue;
+    }
+    HitRecord rec;
+    Object* hit_obj = nullptr;
+    bool hit = false;
+    if (acc == BVH_ACC) hit = s->bvh.Traverse(ray, &hit_obj, rec);
+    else if (acc == GRID_ACC) hit = s->grid.Traverse(ray, &hit_obj, rec);
+    else {  // main.cpp:315-326: linear scan, strict <, first object wins ties
+      for (int k = 0; k < sc.getNumObjects(); k++) {
+        Object* o = sc.getObject((unsigned)k);
+        const HitRecord h = o->hit(ray);
+        if (h.isHit && h.t < rec.t) { rec = h; hit_obj = o; hit = true; }
+      }
+    }
+    t[i] = hit ? rec.t : FLT_MAX;
+    normal[3 * i] = hit ? rec.normal.x : 0.f;
+    normal[3 * i + 1] = hit ? rec.normal.y : 0.f;
+    normal[3 * i + 2] = hit ? rec.normal.z : 0.f;
+    object[i] = hit && hit_obj ? hit_obj->scene_index : -1;
+  }
+  return DRT_OK;
+}
+
+int drt_scene_skybox_color_cpu(const drt_scene* s, const float* dirs, int64_t n, float* rgb) {
+  if (!s || n < 0 || (n && (!dirs || !rgb))) return DRT_E_INVALID;
+  for (int64_t i = 0; i < n; i++) {
+    const Color c = s->scene.GetSkyboxColor(Ray(Vector(0.f, 0.f, 0.f), Vector(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2])));
+    rgb[3 * i] = c.r(); rgb[3 * i + 1] = c.g(); rgb[3 * i + 2] = c.b();
+  }
   return DRT_OK;
 }
 

@@ -1,5 +1,5 @@
 // drt_scene.cpp — host scene model: objects, camera frame, P3F loader, GPU packing.
-#include "drt_scene.hpp"
+#include "../../../include/drt_scene.hpp"
 
 #include <cerrno>
 #include <cstdio>
@@ -367,10 +367,16 @@ bool Scene::load_p3f(const char* name) {
       SetCamera(new Camera(from, at, up, fov, hither, (float)(1000.0 * hither), xres, yres, ar, fr));
     } else if (cmd == "bclr") {
       bgColor = tk.col();
-    } else if (cmd == "env") {
+    } else if (cmd == "env") {  // scene.cpp:687-692: LoadSkybox(token) + SetSkyBoxFlg(true)
       tk.next(tok);
       env_dir = tok;
       SkyBoxFlg = true;
+      if (!LoadSkybox(tok.c_str())) {  // the reference resolves <dir> from the working directory
+        std::string p(name);
+        const size_t cut = p.find_last_of('/');
+        const std::string dir = cut == std::string::npos ? std::string(".") : p.substr(0, cut);
+        LoadSkybox((dir + "/../" + tok).c_str());  // else next to P3D_Scenes/
+      }
     } else if (!cmd.empty() && cmd[0] == '#') {
       tk.ignore_line();
     } else {

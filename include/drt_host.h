@@ -12,6 +12,12 @@
  *                             grid.cpp:30-97), tree-identical to the reference
  *   drt_scene_upload       <- the hand-off renderScene() relied on through globals
  *                             (main.cpp:79-93): scene + accelerator into a drt_ctx
+ *   drt_scene_load_skybox  <- Scene::LoadSkybox          (scene.cpp:329-378)
+ *   drt_scene_trace_cpu    <- BVH::Traverse / Grid::Traverse on the host (bvh.cpp:231-391,
+ *                             grid.cpp:247-358), the scalar path for CPU callers and tests
+ *   drt_scene_skybox_color_cpu <- Scene::GetSkyboxColor  (scene.cpp:380-458)
+ *
+ * C++ callers use the class API of include/drt_scene.hpp directly (same library).
  *
  * Conventions as in drt.h: 0 / negative drt_status, caller-owned host memory.
  */
@@ -69,6 +75,27 @@ int drt_scene_grid_export(const drt_scene* s, int64_t* cell_start, int32_t* cell
 int drt_scene_camera_frame(const drt_scene* s, drt_camera* out);
 
 int drt_scene_upload(drt_ctx* ctx, drt_scene* s);
+
+/* ---- skybox faces from files (Scene::LoadSkybox, scene.cpp:329-378) ---- */
+/* A decoder for <dir>/<face>.jpg: fills *w, *h, *bpp (3 or 4) and *pixels (malloc'd, rows
+ * top-down; the library frees it and flips to the lower-left origin DevIL gives the reference);
+ * returns 0 on success.  With none registered (or on failure) LoadSkybox reads binary PPM (P6)
+ * <dir>/<face>.ppm.  Process-wide; fn = NULL unregisters. */
+typedef int (*drt_image_decoder)(const char* path, int32_t* w, int32_t* h, int32_t* bpp, uint8_t** pixels,
+                                 void* user);
+int drt_set_image_decoder(drt_image_decoder fn, void* user);
+/* Scene::LoadSkybox(dir) + SetSkyBoxFlg(true); DRT_E_INVALID if a face does not decode. */
+int drt_scene_load_skybox(drt_scene* s, const char* dir);
+
+/* ---- the scalar host path (include/drt_scene.hpp), one ray at a time on the CPU ---- */
+/* BVH::Traverse / Grid::Traverse (bvh.cpp:231-391, grid.cpp:247-358) or the NONE scan
+ * (main.cpp:315-326, :430-441) of the built scene for n rays {ox,oy,oz,dx,dy,dz}: closest fills
+ * t (FLT_MAX on a miss), normal (n x 3) and object (scene index, -1 on a miss); shadow fills
+ * occluded with the accelerator's own range rule.  DRT_E_STATE before drt_scene_build. */
+int drt_scene_trace_cpu(const drt_scene* s, int shadow, const float* rays, int64_t n, float* t, float* normal,
+                        int32_t* object, uint8_t* occluded);
+/* Scene::GetSkyboxColor (scene.cpp:380-458) for n directions -> n x 3 floats. */
+int drt_scene_skybox_color_cpu(const drt_scene* s, const float* dirs, int64_t n, float* rgb);
 
 /* ---- output image ---- */
 /* u8fromfloat (maths.h:126-130: x*255.99f >= 255 ? 255 : (uint8_t)(x*255.99f), negatives -> 0)

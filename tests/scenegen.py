@@ -146,3 +146,13 @@ def balls_low_text(res=(512, 512), spp=16, accel="none"):
                      ("-" + b, "-" + c, z), (e, "-" + d, "0.544331"), ("-" + c, "-" + b, z), (f, "-" + f, z)):
         lines.append(f"s {x} {y} {zz} {r}")
     return "\n".join(lines) + "\n"
+
+
+def set_accel(text, accel):
+    """The same P3F text with its `accel` command set to `accel` (added if absent)."""
+    lines = text.split("\n")
+    for i, l in enumerate(lines):
+        if l.split()[:1] == ["accel"]:
+            lines[i] = f"accel {accel}"
+            return "\n".join(lines)
+    return f"accel {accel}\n" + text

@@ -210,3 +210,23 @@ def test_shipped_scene_fixture_loads_like_oracle(oracle_mod, tmp_path, scene):
     for k in ("leaf", "index", "nobjs", "order"):
         np.testing.assert_array_equal(x[k], y[k], err_msg=k)
     np.testing.assert_array_equal(bits(x["boxes"]), bits(y["boxes"]))
+
+
+@pytest.mark.parametrize("case,accel", [("mixed", "bvh"), ("tris2k", "bvh"), ("mixed", "grid"), ("tris2k", "grid")])
+def test_scalar_cpu_traverse_matches_reference_golden(tmp_path, case, accel):
+    """drt_scene_trace_cpu: the host BVH::Traverse / Grid::Traverse (one ray at a time on the CPU,
+    no device) return the reference's results bit for bit."""
+    g = np.load(GOLD / f"ref_{case}.npz")
+    p = tmp_path / "s.p3f"
+    p.write_bytes(g["scene_text"].tobytes())
+    s = drt.Scene.load_p3f(p)
+    s.set_accel(accel)
+    s.build()
+    pre = "bvh" if accel == "bvh" else "grid"
+    rays = g["rays"] if accel == "bvh" else g["grid_rays"]
+    t, n, obj = s.trace_cpu(rays)
+    np.testing.assert_array_equal(obj, g[f"{pre}_obj"])
+    np.testing.assert_array_equal(bits(t), bits(g[f"{pre}_t"]))
+    np.testing.assert_array_equal(bits(n), bits(g[f"{pre}_n"]))
+    srays = g["shadow_rays"] if accel == "bvh" else g["grid_rays"]
+    np.testing.assert_array_equal(s.trace_cpu(srays, shadow=True), g[f"{pre}_occ"])
