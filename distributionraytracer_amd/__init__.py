@@ -20,7 +20,7 @@ import numpy as np
 from . import _lib
 from ._lib import ACCEL, FRAME_STATS, DrtCamera, DrtFrameParams, DrtFrameStats, DrtOptions, DrtSceneInfo, check
 
-__all__ = ["Scene", "Renderer", "ACCEL", "load_skybox_dir", "SKY_FACES", "build"]
+__all__ = ["Scene", "Renderer", "RendererGroup", "ACCEL", "load_skybox_dir", "SKY_FACES", "build"]
 
 SKY_FACES = ("right", "left", "top", "bottom", "front", "back")  # scene.cpp:333, CubeMap enum
 
@@ -362,3 +362,60 @@ class Renderer:
         s = DrtFrameStats()
         check(_lib.load().drt_trace_stats(self.h, C.byref(s)), self.h, "drt_trace_stats")
         return s.as_dict()
+
+
+class RendererGroup:
+    """Several GPUs behind one handle (drt_group_*, include/drt.h): the scene replicated on every
+    device, each frame tile-sharded over them, all-gathered over RCCL and reassembled on the first
+    device — a single process, no torch.distributed."""
+
+    def __init__(self, devices):
+        L = _lib.load()
+        devs = list(devices)
+        arr = (C.c_int32 * len(devs))(*devs)
+        h = C.c_void_p()
+        rc = L.drt_group_create(C.byref(h), len(devs), arr)
+        if rc != 0:
+            raise RuntimeError(f"drt_group_create({devs}) failed: {_lib.STATUS.get(rc, rc)}")
+        self.h = h
+        self.devices = devs
+        self.scene = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().drt_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed: {_lib.STATUS.get(rc, rc)} "
+                               f"{_lib.load().drt_group_last_error(self.h).decode()}".strip())
+
+    def upload(self, scene: Scene):
+        self._check(_lib.load().drt_group_scene_upload(self.h, scene.h), "drt_group_scene_upload")
+        self.scene = scene
+        return self
+
+    def render(self, seed=1, max_depth=4, roughness=0.0, light_spp=1, progressive_frame=0, accum=None):
+        info = self.scene.info()
+        out = accum if accum is not None else np.zeros((info.res_y, info.res_x, 3), np.float32)
+        p = DrtFrameParams()
+        p.seed, p.max_depth, p.roughness, p.light_spp, p.progressive_frame = seed, max_depth, roughness, light_spp, \
+            progressive_frame
+        self._check(_lib.load().drt_group_render(self.h, C.byref(p), _fp(out)), "drt_group_render")
+        return out
+
+    def render_device(self, d_frame_ptr, seed=1, max_depth=4, roughness=0.0, light_spp=1, stream=None):
+        p = DrtFrameParams()
+        p.seed, p.max_depth, p.roughness, p.light_spp = seed, max_depth, roughness, light_spp
+        self._check(_lib.load().drt_group_render_device(self.h, C.byref(p), C.c_void_p(d_frame_ptr),
+                                                        C.c_void_p(stream or 0)), "drt_group_render_device")
+
+    def synchronize(self):
+        self._check(_lib.load().drt_group_synchronize(self.h), "drt_group_synchronize")

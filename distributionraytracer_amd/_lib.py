@@ -117,7 +117,17 @@ SIGNATURES = {
     "drt_frame_times": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "drt_frame_spans": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double)]),
+    "drt_frame_resolution": (C.c_int, [_vp, _i32]),
+    "drt_group_create": (C.c_int, [C.POINTER(_vp), C.c_int, _i32]),
+    "drt_group_destroy": (None, [_vp]),
+    "drt_group_last_error": (C.c_char_p, [_vp]),
+    "drt_group_size": (C.c_int, [_vp]),
+    "drt_group_ctx": (_vp, [_vp, C.c_int]),
+    "drt_group_render": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _f]),
+    "drt_group_render_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp]),
+    "drt_group_synchronize": (C.c_int, [_vp]),
     # drt_host.h
+    "drt_group_scene_upload": (C.c_int, [_vp, _vp]),
     "drt_scene_new": (_vp, []),
     "drt_scene_load_p3f": (_vp, [C.c_char_p]),
     "drt_scene_free": (None, [_vp]),

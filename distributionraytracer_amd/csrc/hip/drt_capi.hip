@@ -627,6 +627,14 @@ int drt_plan_frame(const drt_ctx* c, const drt_frame_params* p, drt_frame_plan* 
   return DRT_OK;
 }
 
+int drt_frame_resolution(const drt_ctx* c, int32_t res_xy[2]) {
+  if (!c || !res_xy) return DRT_E_INVALID;
+  if (!c->has_scene) return DRT_E_STATE;
+  res_xy[0] = c->cam.res_x;
+  res_xy[1] = c->cam.res_y;
+  return DRT_OK;
+}
+
 int drt_render_device(drt_ctx* c, const drt_frame_params* p, float* d_out, void* stream) {
   if (!c || !p || !d_out) return DRT_E_INVALID;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;

@@ -303,4 +303,16 @@ int upload_scene(drt_ctx* ctx, const Scene& scene, const BVH* bvh, const Grid* g
 
 int render_scene(drt_ctx* ctx, const drt_frame_params& p, float* colors) { return drt_render(ctx, &p, colors); }
 
+int upload_scene(drt_group* g, const Scene& scene, const BVH* bvh, const Grid* grid) {
+  const int n = drt_group_size(g);
+  if (n <= 0) return DRT_E_INVALID;
+  for (int r = 0; r < n; r++) {
+    const int rc = upload_scene(drt_group_ctx(g, r), scene, bvh, grid);
+    if (rc) return rc;
+  }
+  return DRT_OK;
+}
+
+int render_scene(drt_group* g, const drt_frame_params& p, float* colors) { return drt_group_render(g, &p, colors); }
+
 }  // namespace drt

@@ -201,6 +201,16 @@ int drt_scene_upload(drt_ctx* ctx, drt_scene* s) {
   return upload_scene(ctx, s->scene, &s->bvh, &s->grid);
 }
 
+int drt_group_scene_upload(drt_group* g, drt_scene* s) {
+  if (!g || !s) return DRT_E_INVALID;
+  const int n = drt_group_size(g);
+  for (int r = 0; r < n; r++) {  // the scene is replicated on every device
+    const int rc = drt_scene_upload(drt_group_ctx(g, r), s);
+    if (rc) return rc;
+  }
+  return DRT_OK;
+}
+
 int drt_scene_load_skybox(drt_scene* s, const char* dir) {
   if (!s || !dir) return DRT_E_INVALID;
   if (!s->scene.LoadSkybox(dir)) return DRT_E_INVALID;

@@ -186,6 +186,9 @@ typedef struct {
 } drt_frame_plan;
 int drt_plan_frame(const drt_ctx* ctx, const drt_frame_params* params, drt_frame_plan* out);
 
+/* RES_X, RES_Y of the uploaded scene's camera (DRT_E_STATE without a scene). */
+int drt_frame_resolution(const drt_ctx* ctx, int32_t res_xy[2]);
+
 /* Whole frame into host memory (RES_Y*RES_X*3 floats). */
 int drt_render(drt_ctx* ctx, const drt_frame_params* params, float* rgb_out);
 
@@ -231,6 +234,29 @@ int drt_frame_times(drt_ctx* ctx, int max_frames, double* path_ms, double* total
  * oldest frame returned: path-kernel start / end and frame end.  Frames on different streams
  * overlap; the union of their path-kernel spans is the device time the path kernel held. */
 int drt_frame_spans(drt_ctx* ctx, int max_frames, double* path_start, double* path_end, double* frame_end);
+
+/* ---- several GPUs behind one handle (main.cpp:603 is the loop being split) ----
+ * One drt_ctx per device, one HIP stream per device and an RCCL clique over them
+ * (ncclCommInitAll, librccl loaded at run time).  A frame: every device renders its interleaved
+ * 16x16 tiles (shard r of n, the drt_frame_params.shard dealing) into a shard buffer, one
+ * ncclAllGather moves the shards over xGMI, device 0 reassembles the frame.  Upload the scene
+ * to every device's context (drt_group_ctx + drt_upload_*, or drt_group_scene_upload in
+ * drt_host.h).  Progressive frames need a one-device group. */
+typedef struct drt_group drt_group;
+/* devices: n_devices distinct ordinals, or NULL for 0 .. n_devices-1 */
+int drt_group_create(drt_group** out, int n_devices, const int32_t* devices);
+void drt_group_destroy(drt_group* g);
+const char* drt_group_last_error(const drt_group* g);
+int drt_group_size(const drt_group* g);
+drt_ctx* drt_group_ctx(drt_group* g, int rank);
+/* Whole frame into host memory (RES_Y*RES_X*3 floats, row 0 = bottom); blocking.  params:
+ * n_shards 0 or 1 (the group deals the tiles). */
+int drt_group_render(drt_group* g, const drt_frame_params* params, float* rgb_out);
+/* Whole frame into DEVICE memory on device 0 (d_frame: RES_Y*RES_X*3 floats), asynchronous:
+ * device 0's work on `stream0` (NULL = the group's), the other devices' on the group's streams. */
+int drt_group_render_device(drt_group* g, const drt_frame_params* params, float* d_frame, void* stream0);
+/* Wait for every device's stream. */
+int drt_group_synchronize(drt_group* g);
 
 #ifdef __cplusplus
 }

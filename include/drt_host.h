@@ -75,6 +75,8 @@ int drt_scene_grid_export(const drt_scene* s, int64_t* cell_start, int32_t* cell
 int drt_scene_camera_frame(const drt_scene* s, drt_camera* out);
 
 int drt_scene_upload(drt_ctx* ctx, drt_scene* s);
+/* drt_scene_upload to every device of a group (include/drt.h, drt_group_*). */
+int drt_group_scene_upload(drt_group* g, drt_scene* s);
 
 /* ---- skybox faces from files (Scene::LoadSkybox, scene.cpp:329-378) ---- */
 /* A decoder for <dir>/<face>.jpg: fills *w, *h, *bpp (3 or 4) and *pixels (malloc'd, rows

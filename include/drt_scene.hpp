@@ -403,5 +403,9 @@ class Grid {
 // bottom) on the GPU.  Return drt_status codes.
 int upload_scene(drt_ctx* ctx, const Scene& scene, const BVH* bvh, const Grid* grid);
 int render_scene(drt_ctx* ctx, const drt_frame_params& params, float* colors);
+// The same over several GPUs (include/drt.h, drt_group_*): the scene on every device, each frame
+// tile-sharded, all-gathered over RCCL and reassembled on device 0.
+int upload_scene(drt_group* group, const Scene& scene, const BVH* bvh, const Grid* grid);
+int render_scene(drt_group* group, const drt_frame_params& params, float* colors);
 
 }  // namespace drt

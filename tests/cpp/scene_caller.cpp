@@ -24,6 +24,8 @@
 //   sky    SCENE.p3f DIRS.f32 OUT    GetSkyboxColor (skybox from the scene's `env`, LoadSkybox)
 //   hit    SCENE.p3f RAYS.f32 OUT    Object::hit of every object for every ray: {isHit, t, n xyz}
 //   render SCENE.p3f SEED OUT        GPU frame through drt::upload_scene / drt::render_scene
+//   group  SCENE.p3f SEED NDEV OUT   the same frame tile-sharded over NDEV GPUs (drt_group_*:
+//                                    RCCL all-gather, reassembly on device 0), no Python
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -194,6 +196,29 @@ int main(int argc, char** argv) {
         HitRecord h = scene.getObject(k)->hit(r);
         o.put((float)h.isHit); o.put(h.t); o.vec(h.normal);
       }
+  } else if (mode == "group") {
+    Scene scene;
+    if (int rc = load(scene, argv[2])) return rc;
+    BVH bvh;
+    Grid grid;
+    std::vector<Object*> objs = scene.objectList();
+    if (scene.GetAccelStruct() == BVH_ACC) bvh.Build(objs);
+    else if (scene.GetAccelStruct() == GRID_ACC) grid.Build(objs);
+    drt_group* group = nullptr;
+    if (int rc = drt_group_create(&group, atoi(argv[4]), nullptr)) { fprintf(stderr, "drt_group_create: %d\n", rc); return 4; }
+    if (int rc = upload_scene(group, scene, &bvh, &grid)) { fprintf(stderr, "upload_scene: %d\n", rc); return 4; }
+    drt_frame_params p{};
+    p.seed = (uint32_t)strtoul(argv[3], nullptr, 10);
+    p.max_depth = 4;
+    const Camera* cam = scene.GetCamera();
+    std::vector<float> colors((size_t)cam->GetResX() * cam->GetResY() * 3);
+    if (int rc = render_scene(group, p, colors.data())) {
+      fprintf(stderr, "render_scene: %d %s\n", rc, drt_group_last_error(group));
+      return 4;
+    }
+    drt_group_destroy(group);
+    Out o(argv[5]);
+    fwrite(colors.data(), sizeof(float), colors.size(), o.f);
   } else if (mode == "render") {
     Scene scene;
     if (int rc = load(scene, argv[2])) return rc;

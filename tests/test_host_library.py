@@ -230,3 +230,12 @@ def test_scalar_cpu_traverse_matches_reference_golden(tmp_path, case, accel):
     np.testing.assert_array_equal(bits(n), bits(g[f"{pre}_n"]))
     srays = g["shadow_rays"] if accel == "bvh" else g["grid_rays"]
     np.testing.assert_array_equal(s.trace_cpu(srays, shadow=True), g[f"{pre}_occ"])
+
+
+def test_group_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="drt_group_create"):
+        drt.RendererGroup([0])
