@@ -159,6 +159,10 @@ def main():
                     help="frames pipelined on separate streams and scratch slots, so that a frame's start "
                          "overlaps the previous frame's tail (0: 2 on one GPU, 3 on several, where a "
                          "rank's shard is short and the tail a larger share of it)")
+    ap.add_argument("--settle-s", type=float, default=1.0,
+                    help="untimed frames before the warmup steps until this much wall time has passed: the "
+                         "GPU's clocks settle after the idle scene build (measured: with 2 warmup frames the "
+                         "timed frames ran 3 %% slower than the steady 87.8 ms)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
@@ -252,6 +256,19 @@ def main():
     mine = dict(zip(keys, mine.tolist()))
     rays_frame = tot["closest_rays"] + tot["shadow_rays"]
 
+    # clock settle: as many untimed frames as fill --settle-s (one frame timed first; the count is
+    # the max over ranks, since every frame of a multi-rank run holds a collective)
+    settle = 0
+    if args.settle_s > 0:
+        t_s = time.perf_counter()
+        step(shard_ps[0], 0)
+        torch.cuda.synchronize()
+        n_t = torch.tensor([int(args.settle_s / max(1e-3, time.perf_counter() - t_s))], device="cuda")
+        if world > 1:
+            dist.all_reduce(n_t, op=dist.ReduceOp.MAX)
+        settle = 1 + int(n_t.item())
+        for i in range(1, settle):
+            step(shard_ps[i % pipe], i % pipe)
     for i in range(args.warmup):
         step(shard_ps[i % pipe], i % pipe)
     if world > 1:
@@ -348,7 +365,7 @@ def main():
                                + (f", {args.light_spp} quad-light samples" if args.light_spp > 1 else ""),
                    "scene": args.scene, "tris": args.tris if args.scene == "synthetic" else 0, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
                    "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
-                   "frames_in_flight": pipe},
+                   "frames_in_flight": pipe, "settle_frames": settle},
         # bound: the per-CU vector-memory path serving dependent 64-B per-lane record gathers (TA/TD
         # busy 98 %), peak = tools/gather_ceiling.hip's fastest table; achieved =
         # algorithmic record bytes (64 B per inner-node visit + 48 B per primitive test) per second

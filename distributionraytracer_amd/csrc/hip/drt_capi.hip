@@ -638,7 +638,7 @@ int drt_frame_resolution(const drt_ctx* c, int32_t res_xy[2]) {
 int drt_render_device(drt_ctx* c, const drt_frame_params* p, float* d_out, void* stream) {
   if (!c || !p || !d_out) return DRT_E_INVALID;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  const bool full = (p->n_shards <= 1);
+  const bool full = (p->n_shards <= 1) && !(p->flags & DRT_FRAME_SHARD_LAYOUT);
   return run_frame(c, p, d_out, full, st);
 }
 

@@ -191,6 +191,7 @@ int drt_group_render_device(drt_group* g, const drt_frame_params* params, float*
   for (int r = 0; r < g->n; r++) {
     p[r].shard = r;
     p[r].n_shards = g->n;
+    p[r].flags |= DRT_FRAME_SHARD_LAYOUT;  // shard-compact even when n == 1
     int64_t tiles = 0, f = 0;
     const int rc = drt_shard_layout(g->ctx[r], &p[r], &tiles, &f);
     if (rc) G_FAIL(g, rc, "device %d: %s", g->dev[r], drt_last_error(g->ctx[r]));

@@ -45,13 +45,7 @@ int drt_scene_info(const drt_scene* s, drt_scene_info_t* o) {
   o->accel = sc.GetAccelStruct() == BVH_ACC ? DRT_ACCEL_BVH : (sc.GetAccelStruct() == GRID_ACC ? DRT_ACCEL_GRID : DRT_ACCEL_NONE);
   o->n_objects = sc.getNumObjects();
   o->n_lights = sc.getNumLights();
-  drt_scene_desc d;
-  std::vector<drt_prim> p;
-  std::vector<drt_light> l;
-  std::vector<drt_material> m;
-  o->n_materials = 0;
-  sc.describe(d, p, l, m);
-  o->n_materials = (int32_t)m.size();
+  o->n_materials = sc.getNumMaterials();  // (not describe(): that packs every primitive)
   o->has_env = sc.GetSkyBoxFlg() ? 1 : 0;
   o->skybox_loaded = sc.SkyboxComplete() ? 1 : 0;
   o->bvh_nodes = (int32_t)s->bvh.nodeList().size();

@@ -122,7 +122,10 @@ typedef struct {
   uint32_t n_objs;
 } drt_bvh_node;
 
-enum { DRT_FRAME_STATS = 1 };
+/* drt_frame_params.flags: DRT_FRAME_STATS counts rays / node visits / primitive tests;
+ * DRT_FRAME_SHARD_LAYOUT makes drt_render_device write the shard-compact tile buffer of
+ * drt_shard_layout() even for n_shards == 1 (a one-device drt_group) */
+enum { DRT_FRAME_STATS = 1, DRT_FRAME_SHARD_LAYOUT = 2 };
 
 typedef struct {
   uint32_t seed;       /* keyed-RNG seed                                                */

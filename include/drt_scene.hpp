@@ -312,6 +312,7 @@ class Scene {
   void addLight(Light* l) { lights.push_back(l); }  // takes ownership
   Light* getLight(unsigned i) const { return i < lights.size() ? lights[i] : nullptr; }
   Material* addMaterial(const Material& m);
+  int getNumMaterials() const { return (int)materials.size(); }
   // scene.cpp:474-740.  `env <dir>` loads the skybox from <dir> relative to the working
   // directory (the reference's rule), else relative to the scene file's parent directory's
   // parent (P3D_Scenes/../<dir>); if neither decodes, the flag is set and the faces stay empty.
