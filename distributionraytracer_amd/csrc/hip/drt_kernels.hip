@@ -849,6 +849,47 @@ __device__ __forceinline__ bool grid_init(const SceneArgs& S, Lane& L) {
   return true;
 }
 
+// The DDA step of grid.cpp:268-303 / :337-355 as selects, not a three-way branch: the axis whose
+// t_next is smallest (the reference's if / else-if order; NaN falls to z), the closest-hit exit
+// (best.t < that t_next) and one double add on the selected axis — the value the reference's
+// `tx_next += dtx` gives.  A lane with `act` false keeps its state, so the empty-macro-cell walk
+// is a wave-uniform loop (one ballot per iteration) instead of divergent exec-mask bookkeeping:
+// the branchy form spent ~60 SALU per step (SALU 144.5 G vs VALU 97.8 G per frame).  Plain
+// values in and out: selects between lvalues became selects between addresses and put the lane
+// state in scratch.
+struct DdaState {
+  double tx, ty, tz;
+  int ix, iy, iz;
+  bool end, exited;
+};
+struct DdaAxes {
+  double dx, dy, dz;  // dtx, dty, dtz
+  int sx, sy, sz;     // ix_step ...
+  int ex, ey, ez;     // ix_stop ...
+};
+__device__ __forceinline__ double sel3(bool cx, bool cy, double a, double b, double c) {
+  const double r = cy ? b : c;
+  return cx ? a : r;
+}
+__device__ __forceinline__ DdaState dda_step(DdaState d, const DdaAxes& a, bool act, bool shadow, double bt) {
+  const bool cx = d.tx < d.ty && d.tx < d.tz;
+  const bool cy = !cx && d.ty < d.tz;
+  const bool cz = !cx && !cy;
+  const double tsel = sel3(cx, cy, d.tx, d.ty, d.tz);
+  const bool e = act && !shadow && bt < tsel;
+  const bool adv = act && !e;
+  const double tn = tsel + sel3(cx, cy, a.dx, a.dy, a.dz);
+  d.tx = (adv && cx) ? tn : d.tx;
+  d.ty = (adv && cy) ? tn : d.ty;
+  d.tz = (adv && cz) ? tn : d.tz;
+  d.ix += (adv && cx) ? a.sx : 0;
+  d.iy += (adv && cy) ? a.sy : 0;
+  d.iz += (adv && cz) ? a.sz : 0;
+  d.exited = d.exited || (adv && ((cx && d.ix == a.ex) || (cy && d.iy == a.ey) || (cz && d.iz == a.ez)));
+  d.end = d.end || e;
+  return d;
+}
+
 // One cell of Grid::Traverse (grid.cpp:247-306 closest, :309-358 shadow): the cell's objects in
 // insertion order (shadow: any t < |d| ends the query), then the DDA step — closest hits end
 // when best.t < t_next of the stepped axis, leaving the grid is a miss (even with a farther hit).
@@ -896,30 +937,33 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
       return;
     }
   }
+  // the DDA step as selects (dda_step) and the empty-macro-cell walk as a wave-uniform loop
   const float dx = L.q.d.x, dy = L.q.d.y, dz = L.q.d.z;
-  bool end = false, exited = false;
-  auto step = [&]() {
-    if (L.gtx < L.gty && L.gtx < L.gtz) {
-      if (!shadow && (double)L.best_t < L.gtx) end = true;
-      else { L.gtx += L.gdx; ix += (dx > 0.0f) ? 1 : -1; exited = ix == ((dx > 0.0f) ? nx : -1); }
-    } else if (L.gty < L.gtz) {
-      if (!shadow && (double)L.best_t < L.gty) end = true;
-      else { L.gty += L.gdy; iy += (dy > 0.0f) ? 1 : -1; exited = iy == ((dy > 0.0f) ? ny : -1); }
-    } else {
-      if (!shadow && (double)L.best_t < L.gtz) end = true;
-      else { L.gtz += L.gdz; iz += (dz > 0.0f) ? 1 : -1; exited = iz == ((dz > 0.0f) ? nz : -1); }
-    }
-  };
-  step();
+  const int sx = dx > 0.0f ? 1 : -1, sy = dy > 0.0f ? 1 : -1, sz = dz > 0.0f ? 1 : -1;
+  const int ex = dx > 0.0f ? nx : -1, ey = dy > 0.0f ? ny : -1, ez = dz > 0.0f ? nz : -1;
+  const double bt = (double)L.best_t;
+  DdaState d{L.gtx, L.gty, L.gtz, ix, iy, iz, false, false};
+  const DdaAxes ax{L.gdx, L.gdy, L.gdz, sx, sy, sz, ex, ey, ez};
+  d = dda_step(d, ax, true, shadow, bt);
   // Cells of an empty macro-cell hold no object: walk through them here (the same steps and
   // end tests, no memory access) instead of spending a loop iteration and a load on each.
   const int ms = S.gmacro_shift, mx = S.gmacro_dim[0], my = S.gmacro_dim[1];
-  while (!end && !exited) {
-    const uint32_t mi = (uint32_t)(ix >> ms) + (uint32_t)mx * ((uint32_t)(iy >> ms) + (uint32_t)my * (uint32_t)(iz >> ms));
-    if ((macro[mi >> 5] >> (mi & 31u)) & 1u) break;
-    if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
-    step();
+  while (true) {
+    bool act = !d.end && !d.exited;
+    const uint32_t mi = act ? (uint32_t)(d.ix >> ms) + (uint32_t)mx * ((uint32_t)(d.iy >> ms) + (uint32_t)my * (uint32_t)(d.iz >> ms))
+                            : 0u;
+    act = act && !((macro[mi >> 5] >> (mi & 31u)) & 1u);
+    if (__ballot(act) == 0) break;
+    if (STATS && act) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
+    d = dda_step(d, ax, act, shadow, bt);
   }
+  L.gtx = d.tx;
+  L.gty = d.ty;
+  L.gtz = d.tz;
+  ix = d.ix;
+  iy = d.iy;
+  iz = d.iz;
+  const bool end = d.end, exited = d.exited;
   if (end) fl = (fl & ~LF_TRAV) | (L.best_prim != 0xFFFFFFFFu ? LF_HIT : 0u);
   else if (exited) fl &= ~LF_TRAV;
   else L.cur = (uint32_t)ix | ((uint32_t)iy << 10) | ((uint32_t)iz << 20);
@@ -1821,7 +1865,8 @@ static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStrea
 template <bool T, bool ST, int M, int A>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
   // register budget (waves/SIMD); DRT_WAVES=7 measured slower on both accelerators (Grid at 7 / 8
-  // waves: 523 / 446 against 590 Mrays/s at 6)
+  // waves: 523 / 446 against 590 Mrays/s at 6), and so are 5 and 4 (96 / 128 VGPRs, fewer
+  // spills: BVH 1541 / 1422, Grid 593 / 554 against 1770 / 606 at 6)
   if (F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);
   else launch_persistent_w<T, ST, M, 6, A>(S, F, st);
 }

@@ -27,7 +27,7 @@ BUDGET = {
     # Whitted point-light frames on mixed primitives (the shipped Whitted scenes on a BVH)
     "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 65),
     # Grid stepper, AA frames
-    "drt::path_persistent<true, false, 0, 6, 1>": (80, 1852, 6, 245),
+    "drt::path_persistent<true, false, 0, 6, 1>": (80, 1844, 6, 230),
 }
 
 
