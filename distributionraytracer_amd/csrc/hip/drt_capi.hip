@@ -100,7 +100,11 @@ struct drt_ctx {
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
   // batched queries: streaming-query records, primitive results, timing of the last call
   DevBuf d_tq, d_tprim, d_tstats;
-  hipEvent_t tev[2] = {nullptr, nullptr};
+  // tev: streaming-kernel start / end, query done.  Batched queries on one context share these
+  // buffers and the claim counter, so each query waits for the previous one (tev[2]) on its own
+  // stream, and a buffer is only regrown once that query has finished.
+  hipEvent_t tev[3] = {nullptr, nullptr, nullptr};
+  bool trace_issued = false;  // tev[2] has been recorded
   int trace_flags = 0;        // DRT_FRAME_STATS: count traversal work of batched queries
   bool trace_timed = false;   // the last batched query ran the streaming kernel
   bool trace_stats_valid = false;
@@ -586,6 +590,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
     P.F.process_min = env_int("DRT_PROCESS_MIN", 24);
     P.F.waves = env_int("DRT_WAVES", 6);
+    P.F.grid_walk = env_int("DRT_GRID_WALK", 8);  // 2: 1 034, 4: 1 038, 6-8: 1 085, 16: 1 025, uncapped: 693 Mrays/s
   }
   if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
@@ -763,6 +768,11 @@ static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, 
     DRT_HIP(c, hipGetLastError());
     return DRT_OK;
   }
+  if (c->trace_issued) {  // serialise with the previous batched query of this context
+    if (c->d_tq.bytes < 2 * sizeof(float4) * (size_t)n || c->d_tprim.bytes < sizeof(uint32_t) * (size_t)n)
+      DRT_HIP(c, hipEventSynchronize(c->tev[2]));  // about to regrow buffers it may still read
+    DRT_HIP(c, hipStreamWaitEvent(st, c->tev[2], 0));
+  }
   DRT_HIP(c, c->d_tq.ensure(2 * sizeof(float4) * (size_t)n));
   DRT_HIP(c, c->d_tprim.ensure(sizeof(uint32_t) * (size_t)n));
   DRT_HIP(c, c->d_counter.ensure(1024));
@@ -787,6 +797,8 @@ static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, 
   DRT_HIP(c, hipEventRecord(c->tev[1], st));
   if (!shadow) launch_trace_finish(S, q, n, dt, A.prim_out, dn, dobj, st);
   DRT_HIP(c, hipGetLastError());
+  DRT_HIP(c, hipEventRecord(c->tev[2], st));
+  c->trace_issued = true;
   c->trace_timed = true;
   c->trace_stats_valid = stats;
   return DRT_OK;

@@ -215,7 +215,9 @@ int drt_trace_shadow(drt_ctx* ctx, const float* rays, int32_t n, uint8_t* occlud
 /* The same queries on DEVICE buffers, asynchronous on `hip_stream` (NULL = the context's
  * stream): d_rays n x 6 floats; closest fills d_t / d_normal / d_object, shadow d_occluded.
  * BVH scenes run the streaming traversal kernel (one query per lane, lanes refilled as they
- * finish).  Replaces the same BVH/Grid Traverse calls as drt_trace_closest / drt_trace_shadow. */
+ * finish).  Replaces the same BVH/Grid Traverse calls as drt_trace_closest / drt_trace_shadow.
+ * Batched queries of one context are serialised: a query issued on another stream waits (on
+ * the device) for the previous one, whose scratch records and claim counter it reuses. */
 int drt_trace_device(drt_ctx* ctx, int shadow, const float* d_rays, int32_t n, float* d_t, float* d_normal,
                      int32_t* d_object, uint8_t* d_occluded, void* hip_stream);
 /* flags for later batched queries: DRT_FRAME_STATS counts their traversal work */

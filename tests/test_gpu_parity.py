@@ -276,6 +276,26 @@ def test_trace_device_streaming_matches_reference_golden(drt, renderer, tmp_path
     renderer.trace_device(True, srays.data_ptr(), srays.shape[0], d_occluded=occ.data_ptr(), stream=stream)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(occ.cpu().numpy(), g["bvh_occ"])
+    # queries issued back to back on two other streams share the context's query records and
+    # claim counter: the second waits for the first on the device, both stay exact
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    t2 = torch.empty_like(t)
+    obj2 = torch.full_like(obj, -7)
+    occ2 = torch.empty_like(occ)
+    big = rays.repeat(8, 1)  # a larger query first: the next one must not regrow under it
+    tb = torch.empty(big.shape[0], dtype=torch.float32, device="cuda")
+    nb = torch.empty((big.shape[0], 3), dtype=torch.float32, device="cuda")
+    ob = torch.empty(big.shape[0], dtype=torch.int32, device="cuda")
+    renderer.trace_device(False, big.data_ptr(), big.shape[0], tb.data_ptr(), nb.data_ptr(), ob.data_ptr(),
+                          stream=s1.cuda_stream)
+    renderer.trace_device(True, srays.data_ptr(), srays.shape[0], d_occluded=occ2.data_ptr(), stream=s2.cuda_stream)
+    renderer.trace_device(False, rays.data_ptr(), n, t2.data_ptr(), nrm.data_ptr(), obj2.data_ptr(),
+                          stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ob.cpu().numpy(), np.tile(g["bvh_obj"], 8))
+    np.testing.assert_array_equal(occ2.cpu().numpy(), g["bvh_occ"])
+    np.testing.assert_array_equal(obj2.cpu().numpy(), g["bvh_obj"])
+    np.testing.assert_array_equal(bits(t2.cpu().numpy()), bits(g["bvh_t"]))
 
 
 def test_streaming_traverse_many_chunks_matches_oracle(drt, oracle_mod, renderer, tmp_path):
