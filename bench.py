@@ -328,6 +328,7 @@ def main():
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     ceiling = load_ceiling()
     traffic = None
+    valu_busy = None
     dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh", "ks": 0.5}
     extras = [f"{k}{v if isinstance(v, str) else format(v, 'g')}" for k, v in ext.items() if v != dflt[k]]
     head = f"tris{args.tris}" if args.scene == "synthetic" else args.scene
@@ -338,6 +339,12 @@ def main():
             tr = json.loads(tj.read_text())
             if tr.get("workload") == workload_key:
                 traffic = tr.get("hbm_bytes_per_launch")
+                # VALU busy against the gfx950 issue peak: a wave64 VALU instruction occupies a
+                # SIMD for 2 cycles (32 lanes/cycle: 157 TFLOP/s f32 = 1024 SIMDs x 2.4 GHz x 32 x
+                # 2); kernel cycles = GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs)
+                raw = tr.get("raw", {})
+                if raw.get("SQ_INSTS_VALU") and raw.get("GRBM_GUI_ACTIVE"):
+                    valu_busy = 2.0 * raw["SQ_INSTS_VALU"] / (1024.0 * raw["GRBM_GUI_ACTIVE"] / 8.0)
         except Exception:
             traffic = None
 
@@ -375,6 +382,7 @@ def main():
                      "frac": round(achieved / ceiling["peak_GB_per_s"], 4) if ceiling else None,
                      "traffic": traffic,
                      "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                     "valu_busy": round(valu_busy, 4) if valu_busy else None,
                      "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),
                      "ceiling": ceiling},

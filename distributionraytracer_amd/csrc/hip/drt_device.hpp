@@ -17,6 +17,23 @@
 namespace drt {
 
 // ------------------------------------------------------------------------------------------
+// 1.0f / a, correctly rounded.  For 2^-125 <= |a| <= 2^125, v_rcp_f32 (<= 1 ulp) refined by one
+// FMA Newton step (e = 1 - a*r exact, r + r*e) rounds correctly for EVERY input: checked
+// exhaustively on gfx950 against the IEEE division over all 2^32 bit patterns (tools/rcp_check.hip,
+// 0 mismatches, profiles/r02_rcp_check.json).  Three VALU instead of the ~10 of hipcc's
+// div_scale / div_fmas / div_fixup expansion.  Zeros, infinities, NaNs and the reciprocals that
+// would be denormal or overflow take the full division (a branch that no wave takes in practice).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rcp_rn(float a) {
+  const float m = __builtin_fabsf(a);
+  if (__builtin_expect(m >= 0x1p-125f && m <= 0x1p125f, 1)) {
+    const float r = __builtin_amdgcn_rcpf(a);
+    return __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);
+  }
+  return 1.0f / a;
+}
+
+// ------------------------------------------------------------------------------------------
 // Vector / Color (vector.cpp:4-102, color.h:38-75)
 // ------------------------------------------------------------------------------------------
 struct V3 {
@@ -158,7 +175,7 @@ __device__ __forceinline__ bool hit_triangle(const float4& q0, const float4& q1,
   V3 v0 = mk(q0.x, q0.y, q0.z), e1 = mk(q1.x, q1.y, q1.z), e2 = mk(q2.x, q2.y, q2.z);
   V3 h = cross(r.d, e2);
   float a = dot(e1, h);
-  float f = 1.0f / a;
+  float f = rcp_rn(a);  // scene.cpp:56: f = 1.0/a
   V3 s = sub(r.o, v0);
   float u = f * dot(s, h);
   if (u < 0.0f || u > 1.0f) return false;
@@ -224,7 +241,7 @@ __device__ __forceinline__ bool hit_triangle_sel(const float4& q0, const float4&
   V3 v0 = mk(q0.x, q0.y, q0.z), e1 = mk(q1.x, q1.y, q1.z), e2 = mk(q2.x, q2.y, q2.z);
   V3 h = cross(r.d, e2);
   float a = dot(e1, h);
-  float f = 1.0f / a;
+  float f = rcp_rn(a);  // scene.cpp:56: f = 1.0/a
   V3 s = sub(r.o, v0);
   float u = f * dot(s, h);
   V3 q = cross(s, e1);
