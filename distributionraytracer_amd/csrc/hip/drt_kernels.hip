@@ -1890,9 +1890,15 @@ static void launch_persistent_w(const SceneArgs& S, const FrameArgs& F, hipStrea
 }
 template <bool T, bool ST, int M, int A>
 static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStream_t st) {
-  // register budget (waves/SIMD); DRT_WAVES=7 measured slower on both accelerators (Grid at 7 / 8
-  // waves: 523 / 446 against 590 Mrays/s at 6), and so are 5 and 4 (96 / 128 VGPRs, fewer
-  // spills: BVH 1541 / 1422, Grid 593 / 554 against 1770 / 606 at 6)
+  // register budget (waves/SIMD, DRT_WAVES).  BVH: 6 (80 VGPRs); 7 measured slower, and so were 5
+  // and 4 (BVH 1541 / 1422 against 1770 Mrays/s at 6).  Grid: 5 (96 VGPRs) since its empty-cell
+  // walk is capped per call (round 2: 1 101-1 177 against 1 039-1 085 at 6, interleaved runs;
+  // 4 waves 983, 7 waves 880)
+  if (A == ACC_GRID) {
+    if (F.waves == 6) launch_persistent_w<T, ST, M, 6, A>(S, F, st);
+    else launch_persistent_w<T, ST, M, 5, A>(S, F, st);
+    return;
+  }
   if (F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);
   else launch_persistent_w<T, ST, M, 6, A>(S, F, st);
 }

@@ -104,7 +104,7 @@ struct FrameArgs {
   unsigned int* work_counter;  // persistent kernel: next unclaimed work item (zeroed per frame)
   int refill_min;              // persistent kernel: refill a wave once this many lanes are idle
   int process_min;             // persistent kernel: shade once this many lanes have a result
-  int waves;                   // persistent kernel: register budget (waves per SIMD: 6 or 7)
+  int waves;                   // persistent kernel: register budget (waves per SIMD: BVH 6 or 7, Grid 5 or 6)
   int grid_walk;               // Grid persistent kernel: empty-macro-cell steps per call
   uint32_t part_items;         // persistent kernel: items per XCD work partition (ceil(n_items / 8))
   const uint8_t* perm;         // persistent kernel, AA / in-order frames: shuffle_kernel's slot -> sample map

@@ -26,8 +26,8 @@ BUDGET = {
     "drt::path_persistent<true, false, 1, 6, 2>": (80, 2416, 6, 106),
     # Whitted point-light frames on mixed primitives (the shipped Whitted scenes on a BVH)
     "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 65),
-    # Grid stepper, AA frames
-    "drt::path_persistent<true, false, 0, 6, 1>": (80, 1844, 6, 230),
+    # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs)
+    "drt::path_persistent<true, false, 0, 5, 1>": (96, 1844, 5, 230),
 }
 
 
