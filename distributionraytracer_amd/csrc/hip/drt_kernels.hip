@@ -748,7 +748,8 @@ enum LaneFlag : uint32_t {
   LF_POP = 8u,      // next node step starts with a pop attempt
   LF_FINITE = 16u,  // ray origin and (float)(1.0/d) are all finite
   LF_OUTSIDE = 32u, // shading state: the hit was on the outside of the surface (main.cpp:364)
-  LF_EMPTY = 64u    // Grid: the current cell lies in an empty macro-cell (no range load needed)
+  LF_EMPTY = 64u,   // Grid: the current cell lies in an empty macro-cell (no range load needed)
+  LF_INCELL = 128u  // Grid: objects of the current cell left, from record L.spa on
 };
 
 struct Lane {
@@ -898,16 +899,18 @@ __device__ __forceinline__ DdaState dda_step(DdaState d, const DdaAxes& a, bool 
 // objects with the next cell's range prefetched speculatively — 6-17 % slower than a whole cell
 // per iteration.)
 template <bool TRI_ONLY, bool STATS>
-__device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters& C, const LdsU32* macro, int walk) {
+__device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters& C, const LdsU32* macro, int walk,
+                                          int pairs) {
   uint32_t fl = L.fl;
   const bool shadow = (fl & LF_SHADOW) != 0u;
   const int nx = S.gdim[0], ny = S.gdim[1], nz = S.gdim[2];
   int ix = (int)(L.cur & 1023u), iy = (int)((L.cur >> 10) & 1023u), iz = (int)(L.cur >> 20);
-  if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
+  const bool resume = (fl & LF_INCELL) != 0u;  // the cell's objects from the cursor on
+  if (STATS && !resume) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
   const size_t cidx = (size_t)ix + (size_t)nx * iy + (size_t)nx * ny * iz;
   uint32_t b = 0, e = 0;  // LF_EMPTY: the cell lies in an empty macro-cell (the last call's walk)
   if (!(fl & LF_EMPTY)) {
-    b = S.cell_start[cidx];
+    b = resume ? L.spa : S.cell_start[cidx];
     e = S.cell_start[cidx + 1];
   }
   // the cell's objects in insertion order, two inline records (drt_upload_grid) per round trip
@@ -928,7 +931,17 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
 #ifdef DRT_GRID_DIAG
   if (STATS) C.v[ST_CYC_LEAF]++;  // lane cell visits (grid_step calls)
 #endif
-  for (uint32_t q = b; q < e; q += 2) {
+  // At most `pairs` round trips per call, for the same reason as the walk's cap below: a lane in
+  // a crowded cell would keep the wave in this loop while the others wait.  It stays in the cell
+  // (LF_INCELL, the next record in L.spa, which the Grid stepper does not otherwise use) and goes
+  // on in the next call.
+  bool stay = false;
+  for (uint32_t q = b, k = 0; q < e; q += 2, k++) {
+    if (k == (uint32_t)pairs) {
+      stay = true;
+      L.spa = q;
+      break;
+    }
 #ifdef DRT_GRID_DIAG
     if (STATS && wave_leader()) C.v[ST_WAVE_LEAF_ITERS]++;  // pair-loop wave iterations
 #endif
@@ -955,7 +968,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   const double bt = (double)L.best_t;
   DdaState d{L.gtx, L.gty, L.gtz, ix, iy, iz, false, false};
   const DdaAxes ax{L.gdx, L.gdy, L.gdz, sx, sy, sz, ex, ey, ez};
-  d = dda_step(d, ax, true, shadow, bt);
+  d = dda_step(d, ax, !stay, shadow, bt);
   // Cells of an empty macro-cell hold no object: walk through them here (the same steps and
   // end tests, no memory access) instead of spending a loop iteration and a load on each.  At most
   // `walk` steps per call: the loop is wave-uniform, and the lanes of a long empty run (a ray
@@ -966,7 +979,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   const int ms = S.gmacro_shift, mx = S.gmacro_dim[0], my = S.gmacro_dim[1];
   bool pending = false;  // stopped by the cap inside an empty macro-cell
   for (int w = 0;; w++) {
-    bool act = !d.end && !d.exited;
+    bool act = !stay && !d.end && !d.exited;
     const uint32_t mi = act ? (uint32_t)(d.ix >> ms) + (uint32_t)mx * ((uint32_t)(d.iy >> ms) + (uint32_t)my * (uint32_t)(d.iz >> ms))
                             : 0u;
     act = act && !((macro[mi >> 5] >> (mi & 31u)) & 1u);
@@ -990,6 +1003,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   iz = d.iz;
   const bool end = d.end, exited = d.exited;
   fl = pending ? (fl | LF_EMPTY) : (fl & ~LF_EMPTY);
+  fl = stay ? (fl | LF_INCELL) : (fl & ~LF_INCELL);
   if (end) fl = (fl & ~LF_TRAV) | (L.best_prim != 0xFFFFFFFFu ? LF_HIT : 0u);
   else if (exited) fl &= ~LF_TRAV;
   else L.cur = (uint32_t)ix | ((uint32_t)iy << 10) | ((uint32_t)iz << 20);
@@ -1588,7 +1602,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
     if (trav) {
       if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
       if (ACC == ACC_GRID) {
-        if (in_trav) grid_step<TRI_ONLY, STATS>(S, L, C, (const LdsU32*)lds_bytes, F.grid_walk);
+        if (in_trav) grid_step<TRI_ONLY, STATS>(S, L, C, (const LdsU32*)lds_bytes, F.grid_walk, F.grid_pairs);
       } else {
         const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
         if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);

@@ -106,6 +106,7 @@ struct FrameArgs {
   int process_min;             // persistent kernel: shade once this many lanes have a result
   int waves;                   // persistent kernel: register budget (waves per SIMD: BVH 6 or 7, Grid 5 or 6)
   int grid_walk;               // Grid persistent kernel: empty-macro-cell steps per call
+  int grid_pairs;              // Grid persistent kernel: object-pair round trips per call
   uint32_t part_items;         // persistent kernel: items per XCD work partition (ceil(n_items / 8))
   const uint8_t* perm;         // persistent kernel, AA / in-order frames: shuffle_kernel's slot -> sample map
 };
