@@ -396,8 +396,11 @@ def main():
                                       tot["shadow_leaf"]) / max(1.0, rays_frame), 2),
         "setup_s": round(build_s, 2),
         # fraction of lanes doing useful work in the node loop / in the path loop (wave64)
+        # (Grid: a wave iteration also walks empty cells, several per lane, so visits per wave
+        # iteration is not a lane fraction there; tools/grid_diag.py has the Grid's own counters)
         "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
-                                         tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3),
+                                         tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3)
+                     if args.accel != "grid" else None,
                      "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3),
                      # BVH leaf block only (the Grid stepper has no separate leaf block)
                      "leaf_block": round((tot["closest_leaf"] + tot["shadow_leaf"]) /

@@ -18,6 +18,6 @@ if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
       python3 bench.py --steps $S --warmup $W --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err
   rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  python tools/rocprof_union.py $OUT/prof --steps $S --warmup $W > $OUT/rocprof_union.json || exit $?
+  python tools/rocprof_union.py $OUT/prof --steps $S --warmup $W --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
   cat $OUT/rocprof_union.json
 fi

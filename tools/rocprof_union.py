@@ -4,10 +4,11 @@ computed the way bench.py computes roofline.kernel_ms from HIP events: the union
 dispatches' [start, end] spans divided by K.  Also the mean duration of the serial frames rendered
 after the timed region (roofline.kernel_ms_serial).
 
-Dispatch order of the non-stats path_persistent instantiation in bench.py: W warmup, K timed,
-3 serial, then (one GPU) 2 drt_render frames.
+Dispatch order of the non-stats path_persistent instantiation in bench.py: S clock-settle frames
+(the bench line's config.settle_frames), W warmup, K timed, 3 serial, then (one GPU) 2 drt_render
+frames.
 
-usage: python tools/rocprof_union.py TRACE_DIR --steps K --warmup W
+usage: python tools/rocprof_union.py TRACE_DIR --steps K --warmup W [--settle S | --bench-json F]
 """
 import argparse
 import csv
@@ -24,7 +25,13 @@ def main():
     ap.add_argument("trace_dir")
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--warmup", type=int, required=True)
+    ap.add_argument("--settle", type=int, default=None, help="clock-settle frames before the warmup")
+    ap.add_argument("--bench-json", default=None, help="the profiled run's bench line (settle_frames)")
     a = ap.parse_args()
+    settle = a.settle
+    if settle is None and a.bench_json:
+        settle = json.loads(Path(a.bench_json).read_text())["config"].get("settle_frames", 0)
+    settle = settle or 0
     rows = []
     for f in Path(a.trace_dir).rglob("*kernel_trace.csv"):
         for r in csv.DictReader(open(f)):
@@ -32,10 +39,11 @@ def main():
             if "path_persistent<" in k and k.split("<", 2)[1].split(",")[1].strip() == "false":
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
     rows.sort()
-    timed = rows[a.warmup:a.warmup + a.steps]
-    serial = rows[a.warmup + a.steps:a.warmup + a.steps + 3]
+    w0 = settle + a.warmup
+    timed = rows[w0:w0 + a.steps]
+    serial = rows[w0 + a.steps:w0 + a.steps + 3]
     union_ms = interval_union([s for s, _, _ in timed], [e for _, e, _ in timed]) / 1e6
-    res = {"kernel": timed[0][2] if timed else None, "dispatches": len(rows),
+    res = {"kernel": timed[0][2] if timed else None, "dispatches": len(rows), "settle_frames": settle,
            "kernel_ms_per_step_union": round(union_ms / max(1, len(timed)), 3),
            "kernel_ms_serial_mean": round(sum(e - s for s, e, _ in serial) / max(1, len(serial)) / 1e6, 3),
            "timed_span_ms": round((timed[-1][1] - timed[0][0]) / 1e6, 3) if timed else None}
