@@ -326,6 +326,9 @@ FULL_SIZE = {
     "headline_tri1M_512_64spp": (dict(tris=1_000_000, res=512, spp=64), {}, spread_rows(512, 32)),
     "C4_tri1M_1024_64spp_dof_glossy_depth8": (dict(tris=1_000_000, res=1024, spp=64, aperture=8.0, focal=1.0),
                                               {"roughness": 0.1, "max_depth": 8}, spread_rows(1024, 20)),
+    # the headline scene on the uniform grid (f4): 307 x 307 x 85 cells, 93 % empty, so both caps
+    # of the Grid stepper (empty-cell walk, object pairs per call) are exercised on every row
+    "headline_grid_tri1M_512_64spp": (dict(tris=1_000_000, res=512, spp=64, accel="grid"), {}, spread_rows(512, 16)),
 }
 
 
@@ -337,7 +340,7 @@ def test_full_size_config_matches_oracle(drt, oracle_mod, renderer, case):
 
     sk, kw, rows = FULL_SIZE[case]
     args = types.SimpleNamespace(scene=sk.get("scene", "synthetic"), res=sk["res"], spp=sk["spp"])
-    ext = {"aperture": sk.get("aperture", 0.0), "focal": sk.get("focal", 1.0), "accel": "bvh", "ks": 0.5}
+    ext = {"aperture": sk.get("aperture", 0.0), "focal": sk.get("focal", 1.0), "accel": sk.get("accel", "bvh"), "ks": 0.5}
     tris = bench.synthetic_triangles(sk["tris"], 1) if "tris" in sk else None
     a = bench.make_scene(drt, args, tris, ext)
     a.build()
@@ -497,3 +500,25 @@ def test_frame_plan_routes_huge_frames_to_64bit_kernel(drt, renderer, tmp_path):
     assert plan["work_items"] == 512 * 512 * 64 and plan["persistent"]
     plan = renderer.plan(renderer.frame_params(seed=1, roughness=0.1))  # in-order keyed stream
     assert plan["mode"] == 1 and plan["work_items"] == 512 * 512 and plan["sample_slots"] == 512 * 512 * 64
+
+
+@pytest.mark.parametrize("walk,pairs", [(1, 1), (2, 3), (64, 1 << 20)])
+def test_grid_stepper_caps_do_not_change_the_frame(drt, renderer, monkeypatch, walk, pairs):
+    """The Grid stepper's per-call caps (DRT_GRID_WALK empty cells, DRT_GRID_PAIRS object pairs;
+    grid_step) only reschedule a lane's cells and objects across loop iterations: the frame and the
+    ray / sample counts are identical to the default caps' on the 1M-triangle grid scene."""
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(1_000_000), 128, 4, accel="grid")
+    s.build()
+    renderer.upload(s)
+    ref = renderer.render(seed=11, stats=True)
+    rst = renderer.stats()
+    monkeypatch.setenv("DRT_GRID_WALK", str(walk))
+    monkeypatch.setenv("DRT_GRID_PAIRS", str(pairs))
+    img = renderer.render(seed=11, stats=True)
+    st = renderer.stats()
+    np.testing.assert_array_equal(bits(img), bits(ref))
+    for k in ("closest_rays", "shadow_rays", "closest_leaf", "shadow_leaf", "closest_prims", "shadow_prims", "samples"):
+        assert st[k] == rst[k], k
