@@ -124,12 +124,20 @@ def interval_union(starts, ends):
     return tot
 
 
-def load_ceiling():
-    """The measured gather ceiling (profiles/gather_ceiling.json): the fastest table's rate."""
+def load_ceiling(working_set=None):
+    """The measured gather ceiling (profiles/gather_ceiling.json): the fastest table's rate (the
+    bound), and the rate for the smallest measured table that holds the scene's records (one chain
+    per lane, as the path kernel runs) as a same-size reference."""
     try:
         c = json.loads(CEILING_JSON.read_text())
-        return {"peak_GB_per_s": c["peak_GB_per_s"], "table_bytes": c["peak_table_bytes"],
-                "source": "profiles/gather_ceiling.json (tools/gather_ceiling.hip)"}
+        out = {"peak_GB_per_s": c["peak_GB_per_s"], "table_bytes": c["peak_table_bytes"],
+               "source": "profiles/gather_ceiling.json (tools/gather_ceiling.hip)"}
+        rows = sorted((r for r in c.get("rows", []) if r.get("chains") == 1), key=lambda r: r["table_bytes"])
+        if working_set and rows:
+            fit = next((r for r in rows if r["table_bytes"] >= working_set), rows[-1])
+            out["same_size"] = {"table_bytes": fit["table_bytes"], "GB_per_s": fit["GB_per_s"],
+                                "scene_record_bytes": int(working_set)}
+        return out
     except Exception:
         return None
 
@@ -326,7 +334,10 @@ def main():
     bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-    ceiling = load_ceiling()
+    # the scene's records: inner BVH nodes (64 B; a binary tree has (nodes - 1) / 2 of them) and
+    # primitives (48 B)
+    ceiling = load_ceiling(64 * max(0, (info.bvh_nodes - 1) // 2) + 48 * info.n_objects
+                           if args.accel == "bvh" else None)
     traffic = None
     valu_busy = None
     dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh", "ks": 0.5}
@@ -380,6 +391,8 @@ def main():
         "roofline": {"bound": "vmem_gather", "achieved": round(achieved, 1),
                      "peak": ceiling["peak_GB_per_s"] if ceiling else None, "unit": "GB/s",
                      "frac": round(achieved / ceiling["peak_GB_per_s"], 4) if ceiling else None,
+                     "frac_same_size": round(achieved / ceiling["same_size"]["GB_per_s"], 4)
+                     if ceiling and "same_size" in ceiling else None,
                      "traffic": traffic,
                      "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                      "valu_busy": round(valu_busy, 4) if valu_busy else None,
