@@ -108,6 +108,15 @@ struct drt_ctx {
   int trace_flags = 0;        // DRT_FRAME_STATS: count traversal work of batched queries
   bool trace_timed = false;   // the last batched query ran the streaming kernel
   bool trace_stats_valid = false;
+  // A frame's shuffle and reduce kernels run on a high-priority auxiliary stream per slot, linked
+  // to the caller's stream by events: with frames in flight, the persistent kernels of the other
+  // frames hold every CU, and on the caller's stream these small kernels queued behind their
+  // pending blocks for milliseconds, stalling the next frame of that stream (kernel trace of
+  // 8-way shard frames).  ev_path marks the slot's last path kernel (the next
+  // shuffle of that slot rewrites the permutation it reads).
+  hipStream_t aux[DRT_FRAME_SLOTS] = {};
+  hipEvent_t ev_shuf[DRT_FRAME_SLOTS] = {}, ev_path[DRT_FRAME_SLOTS] = {}, ev_red[DRT_FRAME_SLOTS] = {};
+  bool path_issued[DRT_FRAME_SLOTS] = {};
 };
 
 #define DRT_FAIL(ctx, code, ...)                                        \
@@ -182,6 +191,17 @@ int drt_create(drt_ctx** out, const drt_options* opt) {
       drt_destroy(c);
       return DRT_E_HIP;
     }
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  for (int k = 0; k < DRT_FRAME_SLOTS; k++) {
+    if (hipStreamCreateWithPriority(&c->aux[k], hipStreamNonBlocking, greatest) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_shuf[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_path[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_red[k], hipEventDisableTiming) != hipSuccess) {
+      drt_destroy(c);
+      return DRT_E_HIP;
+    }
+  }
   *out = c;
   return DRT_OK;
 }
@@ -194,6 +214,14 @@ void drt_destroy(drt_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->tev)
     if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < DRT_FRAME_SLOTS; k++) {
+    if (c->aux[k]) {
+      (void)hipStreamSynchronize(c->aux[k]);
+      (void)hipStreamDestroy(c->aux[k]);
+    }
+    for (hipEvent_t e : {c->ev_shuf[k], c->ev_path[k], c->ev_red[k]})
+      if (e) (void)hipEventDestroy(e);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -571,12 +599,19 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // per-pixel sample shuffle, once per pixel instead of once per sample (spp < 2: no shuffle); ahead
   // of the frame's first event, so that the path-kernel time is the persistent kernel's own
   const bool shuffled = P.F.mode == MODE_AA || (P.F.mode == MODE_SEQ && P.F.spp > 0);
+  const bool use_aux = env_int("DRT_AUX_STREAMS", 1) != 0;
+  hipStream_t ax = use_aux ? c->aux[slot] : st;
   if (P.persistent && shuffled && P.F.spp >= 2 && P.F.spp <= 256 && P.F.n_items && env_int("DRT_PERM", 1)) {
     DevBuf& d_perm = c->d_perm_s[slot];
     DRT_HIP(c, d_perm.ensure((size_t)P.F.n_my_tiles * P.F.tile * P.F.tile * P.F.spp));
-    launch_shuffle(P.F, c->cam.res_x, c->cam.res_y, d_perm.as<uint8_t>(), st);
+    if (use_aux && c->path_issued[slot]) DRT_HIP(c, hipStreamWaitEvent(ax, c->ev_path[slot], 0));
+    launch_shuffle(P.F, c->cam.res_x, c->cam.res_y, d_perm.as<uint8_t>(), ax);
     P.F.perm = d_perm.as<uint8_t>();
     DRT_HIP(c, hipGetLastError());
+    if (use_aux) {
+      DRT_HIP(c, hipEventRecord(c->ev_shuf[slot], ax));
+      DRT_HIP(c, hipStreamWaitEvent(st, c->ev_shuf[slot], 0));
+    }
   }
   hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
   c->frames++;
@@ -599,8 +634,19 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   }
   DRT_HIP(c, hipGetLastError());
   DRT_HIP(c, hipEventRecord(ev[1], st));
-  if (P.F.n_my_tiles) launch_reduce(P.R, st);
-  DRT_HIP(c, hipGetLastError());
+  if (use_aux) {
+    DRT_HIP(c, hipEventRecord(c->ev_path[slot], st));
+    c->path_issued[slot] = true;
+  }
+  if (P.F.n_my_tiles) {
+    if (use_aux) DRT_HIP(c, hipStreamWaitEvent(ax, c->ev_path[slot], 0));
+    launch_reduce(P.R, ax);
+    DRT_HIP(c, hipGetLastError());
+    if (use_aux) {
+      DRT_HIP(c, hipEventRecord(c->ev_red[slot], ax));
+      DRT_HIP(c, hipStreamWaitEvent(st, c->ev_red[slot], 0));
+    }
+  }
   DRT_HIP(c, hipEventRecord(ev[2], st));
   return DRT_OK;
 }
