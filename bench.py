@@ -196,7 +196,10 @@ def main():
     torch.cuda.set_device(dev)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            # RCCL's all-gather kernel needs CU room like any kernel: on a high-priority stream it
+            # is dispatched ahead of the other frames' pending persistent blocks
+            opts = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev), pg_options=opts)
         else:
             dist.init_process_group(backend)
 
