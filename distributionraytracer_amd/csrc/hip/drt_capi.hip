@@ -117,6 +117,11 @@ struct drt_ctx {
   hipStream_t aux[DRT_FRAME_SLOTS] = {};
   hipEvent_t ev_shuf[DRT_FRAME_SLOTS] = {}, ev_path[DRT_FRAME_SLOTS] = {}, ev_red[DRT_FRAME_SLOTS] = {};
   bool path_issued[DRT_FRAME_SLOTS] = {};
+  // The auxiliary streams cost each frame ~0.17 ms of cross-stream event latency, which only
+  // pays for itself on long frames: they are used once a completed frame's path kernel took
+  // >= kAuxMinMs (DRT_AUX_STREAMS=0 / 1 forces them off / on).  -1 = no completed frame yet.
+  static constexpr double kAuxMinMs = 4.0;
+  double last_path_ms = -1.0;
 };
 
 #define DRT_FAIL(ctx, code, ...)                                        \
@@ -570,6 +575,18 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   return DRT_OK;
 }
 
+// Path-kernel time of the newest frame whose path kernel has finished (no waiting).
+static void note_last_path_ms(drt_ctx* c) {
+  const uint64_t look = std::min<uint64_t>(c->frames, 4);
+  for (uint64_t k = 0; k < look; k++) {
+    hipEvent_t* ev = &c->ring[3 * ((c->frames - 1 - k) % drt_ctx::kRing)];
+    if (hipEventQuery(ev[1]) != hipSuccess) continue;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) c->last_path_ms = ms;
+    return;
+  }
+}
+
 static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool full_frame, hipStream_t st) {
   Plan P;
   int rc = plan_frame(c, p, P);
@@ -599,7 +616,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // per-pixel sample shuffle, once per pixel instead of once per sample (spp < 2: no shuffle); ahead
   // of the frame's first event, so that the path-kernel time is the persistent kernel's own
   const bool shuffled = P.F.mode == MODE_AA || (P.F.mode == MODE_SEQ && P.F.spp > 0);
-  const bool use_aux = env_int("DRT_AUX_STREAMS", 1) != 0;
+  const int aux_mode = env_int("DRT_AUX_STREAMS", -1);
+  if (aux_mode < 0) note_last_path_ms(c);
+  const bool use_aux = aux_mode > 0 || (aux_mode < 0 && c->last_path_ms >= drt_ctx::kAuxMinMs);
   hipStream_t ax = use_aux ? c->aux[slot] : st;
   if (P.persistent && shuffled && P.F.spp >= 2 && P.F.spp <= 256 && P.F.n_items && env_int("DRT_PERM", 1)) {
     DevBuf& d_perm = c->d_perm_s[slot];
