@@ -410,24 +410,28 @@ def test_no_lights_and_deepest_recursion_match_oracle(drt, oracle_mod, renderer,
         compare_images(img, ref)
 
 
-@pytest.mark.parametrize("pipe", [2, 4])
-def test_pipelined_slots_match_sequential_frame(drt, renderer, tmp_path, pipe):
+@pytest.mark.parametrize("pipe,aux", [(2, "0"), (2, "1"), (4, "1")])
+def test_pipelined_slots_match_sequential_frame(drt, renderer, tmp_path, monkeypatch, pipe, aux):
     """Frames in flight (scratch slots 0 .. pipe-1, one stream each, bench.py --frames-in-flight)
-    give the frame a lone render gives, bit for bit; a slot outside DRT_FRAME_SLOTS is refused."""
+    give the frames lone renders give, bit for bit, with and without the auxiliary shuffle /
+    reduce streams (DRT_AUX_STREAMS; every frame has its own seed, so a permutation or sample
+    buffer reused too early would show); a slot outside DRT_FRAME_SLOTS is refused."""
     import torch
 
     p = sg.write(tmp_path, "s.p3f", sg.synthetic_scene_text(20000, res=(64, 48), spp=16))
     s = drt.Scene.load_p3f(p)
     renderer.upload(s)
-    whole = renderer.render(seed=21)
+    n = 3 * pipe
+    lone = [renderer.render(seed=21 + i) for i in range(n)]
+    monkeypatch.setenv("DRT_AUX_STREAMS", aux)
     streams = [torch.cuda.Stream() for _ in range(pipe)]
-    outs = [torch.zeros((48, 64, 3), dtype=torch.float32, device="cuda") for _ in range(pipe)]
-    for i in range(3 * pipe):
+    outs = [torch.zeros((48, 64, 3), dtype=torch.float32, device="cuda") for _ in range(n)]
+    for i in range(n):
         j = i % pipe
-        renderer.render_device(renderer.frame_params(seed=21, slot=j), outs[j].data_ptr(), streams[j].cuda_stream)
+        renderer.render_device(renderer.frame_params(seed=21 + i, slot=j), outs[i].data_ptr(), streams[j].cuda_stream)
     torch.cuda.synchronize()
-    for o in outs:
-        np.testing.assert_array_equal(o.cpu().numpy().view(np.uint32), whole.view(np.uint32))
+    for i in range(n):
+        np.testing.assert_array_equal(outs[i].cpu().numpy().view(np.uint32), lone[i].view(np.uint32))
     with pytest.raises(RuntimeError, match="slot"):
         renderer.render_device(renderer.frame_params(seed=21, slot=4), outs[0].data_ptr(), streams[0].cuda_stream)
 
