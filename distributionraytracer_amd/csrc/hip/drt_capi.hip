@@ -644,8 +644,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
     P.F.process_min = env_int("DRT_PROCESS_MIN", 24);
     P.F.waves = env_int("DRT_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 6);
-    P.F.grid_pairs = env_int("DRT_GRID_PAIRS", 3);
-    P.F.grid_walk = env_int("DRT_GRID_WALK", 5);  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
+    P.F.grid_pairs = std::max(1, env_int("DRT_GRID_PAIRS", 3));  // >= 1: a lane must make progress
+    P.F.grid_walk = std::max(0, env_int("DRT_GRID_WALK", 5));  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
   if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
