@@ -95,6 +95,9 @@ struct drt_ctx {
   // frame scratch per slot (drt_frame_params.slot): frames on different slots may be in flight
   // together on different streams
   DevBuf d_samples_s[DRT_FRAME_SLOTS], d_stats_s[DRT_FRAME_SLOTS], d_counter_s[DRT_FRAME_SLOTS], d_perm_s[DRT_FRAME_SLOTS];
+  // MODE_SEQ tail continuation slots per frame slot (FrameArgs::seq_cont), one per resident lane
+  DevBuf d_cont_s[DRT_FRAME_SLOTS];
+  int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
   bool stats_valid = false;  // the last frame ran with DRT_FRAME_STATS
@@ -645,7 +648,19 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     P.F.process_min = env_int("DRT_PROCESS_MIN", 24);
     P.F.waves = env_int("DRT_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 6);
     P.F.grid_pairs = std::max(1, env_int("DRT_GRID_PAIRS", 3));  // >= 1: a lane must make progress
-    P.F.grid_walk = std::max(0, env_int("DRT_GRID_WALK", 5));  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
+    P.F.grid_walk = std::max(0, env_int("DRT_GRID_WALK", 5));
+    // MODE_SEQ tail hand-over (DRT_SEQ_DONATE=0: off; DRT_SEQ_SLACK: percent of the waves the
+    // unfinished pixels need that stay, >= 100)
+    if (P.F.mode == MODE_SEQ && env_int("DRT_SEQ_DONATE", 1)) {
+      if (!c->cus) DRT_HIP(c, hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+      const uint32_t cap = (uint32_t)std::max(1, c->cus) * 2048u;  // 32 waves of 64 lanes per CU at most
+      DevBuf& d_cont = c->d_cont_s[slot];
+      DRT_HIP(c, d_cont.ensure(sizeof(unsigned long long) * cap));
+      DRT_HIP(c, hipMemsetAsync(d_cont.p, 0, sizeof(unsigned long long) * cap, st));
+      P.F.seq_cont = d_cont.as<unsigned long long>();
+      P.F.seq_cap = cap;
+      P.F.seq_slack = std::max(100, env_int("DRT_SEQ_SLACK", 100));
+    }  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
   if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);

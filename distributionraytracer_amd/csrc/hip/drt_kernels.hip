@@ -749,7 +749,9 @@ enum LaneFlag : uint32_t {
   LF_FINITE = 16u,  // ray origin and (float)(1.0/d) are all finite
   LF_OUTSIDE = 32u, // shading state: the hit was on the outside of the surface (main.cpp:364)
   LF_EMPTY = 64u,   // Grid: the current cell lies in an empty macro-cell (no range load needed)
-  LF_INCELL = 128u  // Grid: objects of the current cell left, from record L.spa on
+  LF_INCELL = 128u, // Grid: objects of the current cell left, from record L.spa on
+  LF_YIELD = 256u,  // MODE_SEQ tail: the lane's wave is handing its pixels over (set per shading pass)
+  LF_RESUME = 512u  // MODE_SEQ tail: the lane took over a pixel; its next sample starts in finish_sample
 };
 
 struct Lane {
@@ -1248,16 +1250,34 @@ struct FrameStack {
   FrameTail t[kMaxFrames];
 };
 
+// MODE_SEQ tail: hand the rest of the lane's pixel (next sample L.smp, keyed-stream position
+// L.rk) to another wave through a continuation slot.  One 64-bit word per slot, written and read
+// with agent-scope atomics, so no other store has to be ordered before it.  False (the lane goes
+// on itself) when the state does not fit the word or the slots are used up.
+__device__ __forceinline__ bool seq_donate(const FrameArgs& F, const Lane& L) {
+  if (L.smp >= (1u << 12) || L.rk >= (1u << 20)) return false;
+  const uint32_t idx = atomicAdd(F.work_counter + kSeqPush, 1u);
+  if (idx >= F.seq_cap) return false;
+  const unsigned long long v = (unsigned long long)L.item | ((unsigned long long)(L.smp | (L.rk << 12)) << 32);
+  __hip_atomic_store(F.seq_cont + idx, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // rayTracing(depth = 1) returned c: store the sample; MODE_SEQ lanes go on with the pixel's next
-// sample on the same stream.
+// sample on the same stream (or, in a wave handing its pixels over, leave it to another lane).
 template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void finish_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C, V3 c) {
   if (MODE == MODE_SEQ) {  // sample smp of the lane's pixel is done: next sample, same stream
-    F.samples[(size_t)L.item * F.nsub + L.smp] = make_float4(c.x, c.y, c.z, 0.0f);
+    if (!(L.fl & LF_RESUME)) F.samples[(size_t)L.item * F.nsub + L.smp] = make_float4(c.x, c.y, c.z, 0.0f);
     if (++L.smp < (uint32_t)F.nsub) {
+      if ((L.fl & LF_YIELD) && seq_donate(F, L)) {
+        L.item = kNoItem;
+        return;
+      }
       seq_start_sample<STATS, ACC>(S, F, L, C);
       return;
     }
+    if (F.seq_cont) atomicAdd(F.work_counter + kSeqDone, 1u);
     L.item = kNoItem;
     return;
   }
@@ -1272,7 +1292,9 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
   V3 c = mk(0, 0, 0);
   bool after_lights = false;
   const bool hit = (L.fl & LF_HIT) != 0u;
-  if (!(L.fl & LF_SHADOW)) {
+  if (MODE == MODE_SEQ && (L.fl & LF_RESUME)) {
+    // a handed-over pixel: no query result to consume, straight to finish_sample (fsp is 0)
+  } else if (!(L.fl & LF_SHADOW)) {
     if (!hit) {  // main.cpp:351-357
       c = cclamp(background(S, L.q.d));
     } else {
@@ -1462,21 +1484,35 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
   start_query<STATS, ACC>(S, L, r, false, 0.0f, C);
 }
 
+// MODE_SEQ: start pixel `item` at sample smp with its keyed stream at call rk — a pixel just
+// claimed (smp 0, rk past the prologue) or one another wave handed over (seq_donate).  One call
+// site in the persistent loop for both, so the sample start is inlined there once.
+template <bool STATS, int ACC>
+__device__ __forceinline__ void seq_begin(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item, uint32_t smp,
+                                          uint32_t rk, Counters& C) {
+  const Item it = decode_item(F, S.res_x, S.res_y, item, 1);
+  if (!it.valid) {  // padding of a partial tile
+    for (int k = 0; k < F.nsub; k++) F.samples[(size_t)item * F.nsub + k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (F.seq_cont) atomicAdd(F.work_counter + kSeqDone, 1u);
+    L.item = kNoItem;
+    return;
+  }
+  L.item = item;
+  L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+  L.smp = smp;
+  L.rk = rk;
+  seq_start_sample<STATS, ACC>(S, F, L, C);
+}
+__device__ __forceinline__ uint32_t seq_first_rk(const FrameArgs& F) {
+  return F.spp > 0 ? 5u * F.spp - 1u : 0u;  // after the prologue's 4 spp + spp - 1 calls
+}
+
 template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item,
                                           Counters& C) {
   L.item = item;
   if (MODE == MODE_SEQ) {  // work item = pixel
-    const Item it = decode_item(F, S.res_x, S.res_y, item, 1);
-    if (!it.valid) {  // padding of a partial tile
-      for (int k = 0; k < F.nsub; k++) F.samples[(size_t)item * F.nsub + k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      L.item = kNoItem;
-      return;
-    }
-    L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
-    L.smp = 0;
-    L.rk = F.spp > 0 ? 5u * F.spp - 1u : 0u;  // after the prologue's 4 spp + spp - 1 calls
-    seq_start_sample<STATS, ACC>(S, F, L, C);
+    seq_begin<STATS, ACC>(S, F, L, item, 0u, seq_first_rk(F), C);
     return;
   }
   if (MODE == MODE_PROG) {  // work item = pixel, one sample (main.cpp:540-572)
@@ -1562,6 +1598,14 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
   // the claim atomics over 8 words (MI355X_MICROARCH.md, dequeue); measured +0.3 %.
   uint32_t part = __builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u, parts_done = 0;  // HW_REG_XCC_ID
   uint64_t cyc[4] = {0, 0, 0, 0};  // stats builds: refill / node / shading / leaf-block cycles (wave-uniform)
+  // MODE_SEQ tail (F.seq_cont): a lane runs a whole pixel's samples in order, so once every pixel
+  // is claimed the frame's last ~quarter runs on waves whose lanes finish their last pixel at
+  // different times (C4 at 1024^2: 0.56 node-loop SIMD efficiency, against 0.69 at 2048^2 with
+  // 4x the pixels per lane).  Waves numbered past what the unfinished pixels need hand their
+  // pixels over at sample boundaries and exit; the waves kept take them from the slots.
+  // No register is added to the loop for this (its allocation sits on an edge): a
+  // wave handing over sets `part` to 8 (no partition is claimed once the wave is exhausted), and
+  // the unfinished-pixel count is read from memory when it is needed.
   auto stamp = [&]() -> uint64_t {
     if (!STATS) return 0;
     __builtin_amdgcn_sched_barrier(0);
@@ -1587,6 +1631,68 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
       if (L.item == kNoItem) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         if (base + rank < pn) lane_init<STATS, MODE, ACC>(S, F, L, pbeg + base + rank, C);
+      }
+    }
+    if (MODE == MODE_SEQ && exhausted && F.seq_cont && part != 8u) {
+      const uint64_t idle2 = __ballot(L.item == kNoItem);
+      const int n2 = __popcll(idle2);
+      // About one iteration in sixteen (bits of the cycle counter), and on every try of a wave
+      // with nothing to do: is this wave past the number the unfinished pixels need?  Then it
+      // hands its pixels over (part = 8) and exits once they are gone; with no pixel left, every
+      // wave is.  A wave with nothing to do otherwise waits here for a handed-over pixel, so that
+      // the loop's exit test stays the one-line test of the other modes (a test there reading
+      // the pixel count raised the loop's VGPR spills 103 -> 216 and made C4 frames 6x slower).
+      // The shared counters are read sparingly: thousands of waves polling one line slow the
+      // pushes and pops on it.
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      bool look = (now & 0xF000ull) == 0ull;
+      const bool try_pop = n2 == 64 || (n2 >= F.refill_min && (now & 0x3000ull) == 0ull);
+      uint32_t base = 0, k = 0, naps = 0;
+      while (true) {
+        if (look) {
+          const uint32_t left = n_items - __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                              F.work_counter + kSeqDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)(pblock<ACC>() / 64) +
+                                                              (threadIdx.x >> 6));
+          if ((uint64_t)wid * 6400u >= (uint64_t)left * (uint64_t)F.seq_slack) {
+            part = 8u;
+            break;
+          }
+        }
+        if (!try_pop) break;
+        if (lane == 0) {  // take up to n2 handed-over pixels
+          const unsigned long long pp = __hip_atomic_load((unsigned long long*)(F.work_counter + kSeqPush),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t pushed = min((uint32_t)pp, F.seq_cap), popped = (uint32_t)(pp >> 32);
+          if (pushed > popped) {
+            k = min((uint32_t)n2, pushed - popped);
+            if (atomicCAS(F.work_counter + kSeqPop, popped, popped + k) != popped) k = 0;
+            base = popped;
+          }
+        }
+        k = __shfl(k, 0, 64);
+        base = __shfl(base, 0, 64);
+        if (k || n2 != 64) break;
+        __builtin_amdgcn_s_sleep(127);  // ~8 k cycles between tries of an idle wave
+        look = (++naps & 3u) == 0u;
+      }
+      if (k && L.item == kNoItem) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle2, 0u));
+        if (rank < k) {
+          unsigned long long v;  // the slot is written right after its push was counted
+          while ((v = __hip_atomic_load(F.seq_cont + base + rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0ull)
+            __builtin_amdgcn_s_sleep(1);
+          // The lane enters the shading pass as if sample smp - 1 of the pixel had just returned
+          // (LF_RESUME): finish_sample, the one place a pixel's next sample starts, goes on from
+          // there (a second inlined sample start here would cost registers in the loop).
+          L.item = (uint32_t)v;
+          const Item it = decode_item(F, S.res_x, S.res_y, L.item, 1);
+          L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+          L.smp = ((uint32_t)(v >> 32) & 4095u) - 1u;
+          L.rk = (uint32_t)(v >> 44);
+          L.fsp = 0;
+          L.fl = LF_RESUME;
+        }
       }
     }
     const bool live = L.item != kNoItem;
@@ -1621,7 +1727,10 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
         if (done) C.v[ST_LANE_PATH_ITERS]++;
       }
-      if (done) lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
+      if (done) {
+        if (MODE == MODE_SEQ && part == 8u) L.fl |= LF_YIELD;
+        lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
+      }
     }
     if (STATS) {
       const uint64_t t3 = stamp();

@@ -109,7 +109,19 @@ struct FrameArgs {
   int grid_pairs;              // Grid persistent kernel: object-pair round trips per call
   uint32_t part_items;         // persistent kernel: items per XCD work partition (ceil(n_items / 8))
   const uint8_t* perm;         // persistent kernel, AA / in-order frames: shuffle_kernel's slot -> sample map
+  // Persistent kernel, MODE_SEQ frame tail: once every pixel is claimed, waves past the number
+  // the unfinished pixels need hand each pixel's remaining samples over at a sample boundary
+  // (item, next sample, keyed-stream position packed in 64 bits; 0 = slot not yet written) and
+  // exit, so that the next frame's blocks take their CUs.  Null: off.
+  unsigned long long* seq_cont;
+  uint32_t seq_cap;            // continuation slots (one per resident lane bounds the pushes)
+  int seq_slack;               // waves kept = ceil(unfinished pixels * seq_slack / 100 / 64)
 };
+
+// Control words of the MODE_SEQ tail in the per-frame work-counter block (zeroed per frame,
+// after the 8 partition counters): pushes and pops of the continuation slots as one 64-bit
+// pair, and the pixels finished.
+constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 144;
 
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
 struct TraceArgs {

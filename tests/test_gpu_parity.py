@@ -526,3 +526,44 @@ def test_grid_stepper_caps_do_not_change_the_frame(drt, renderer, monkeypatch, w
     np.testing.assert_array_equal(bits(img), bits(ref))
     for k in ("closest_rays", "shadow_rays", "closest_leaf", "shadow_leaf", "closest_prims", "shadow_prims", "samples"):
         assert st[k] == rst[k], k
+
+
+@pytest.mark.parametrize("accel", ["bvh", "grid"])
+def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, monkeypatch, accel):
+    """MODE_SEQ frames (DoF + glossy: a lane runs a pixel's samples in order) hand pixels between
+    waves at sample boundaries once every pixel is claimed (FrameArgs::seq_cont).  A handed-over
+    pixel goes on from the same sample and keyed-stream position, so the frame and every ray /
+    traversal count equal the frame with the hand-over off (DRT_SEQ_DONATE=0), bit for bit, for
+    any number of waves kept (DRT_SEQ_SLACK), on the BVH and the Grid kernel, and with frames in
+    flight on several scratch slots.  The 1M-triangle scene makes the samples long enough for
+    waves to hand pixels over mid-pixel."""
+    import torch
+
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(1_000_000), 192, 16, aperture=8.0, focal=1.0, accel=accel)
+    s.build()
+    renderer.upload(s)
+    kw = {"roughness": 0.1, "max_depth": 8}
+    monkeypatch.setenv("DRT_SEQ_DONATE", "0")
+    ref = renderer.render(seed=13, stats=True, **kw)
+    rst = renderer.stats()
+    monkeypatch.setenv("DRT_SEQ_DONATE", "1")
+    for slack in ("100", "150", "400"):
+        monkeypatch.setenv("DRT_SEQ_SLACK", slack)
+        img = renderer.render(seed=13, stats=True, **kw)
+        st = renderer.stats()
+        np.testing.assert_array_equal(bits(img), bits(ref), err_msg=f"slack {slack}")
+        for k in ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
+                  "closest_prims", "shadow_prims", "samples"):
+            assert st[k] == rst[k], (slack, k)
+    monkeypatch.delenv("DRT_SEQ_SLACK")
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.zeros((192, 192, 3), dtype=torch.float32, device="cuda") for _ in range(4)]
+    for i in range(4):
+        renderer.render_device(renderer.frame_params(seed=13, slot=i % 2, **kw), outs[i].data_ptr(),
+                               streams[i % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for o in outs:
+        np.testing.assert_array_equal(bits(o.cpu().numpy()), bits(ref))
