@@ -118,10 +118,10 @@ struct FrameArgs {
   int seq_slack;               // waves kept = ceil(unfinished pixels * seq_slack / 100 / 64)
 };
 
-// Control words of the MODE_SEQ tail in the per-frame work-counter block (zeroed per frame,
-// after the 8 partition counters): pushes and pops of the continuation slots as one 64-bit
-// pair, and the pixels finished.
-constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 144;
+// Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per
+// frame, after the 8 partition counters): pushes and pops of the continuation slots as one
+// 64-bit pair, and the pixels finished, on a 128-B line of its own (every pixel adds to it).
+constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 192;
 
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
 struct TraceArgs {
