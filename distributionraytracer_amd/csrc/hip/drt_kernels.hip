@@ -1646,7 +1646,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
       // pushes and pops on it.
       const uint64_t now = __builtin_amdgcn_s_memtime();
       bool look = (now & 0xF000ull) == 0ull;
-      const bool try_pop = n2 == 64 || (n2 >= F.refill_min && (now & 0x3000ull) == 0ull);
+      const bool try_pop = n2 == 64 || (n2 >= F.seq_pop_min && (now & 0x3000ull) == 0ull);
       uint32_t base = 0, k = 0, naps = 0;
       while (true) {
         if (look) {

@@ -22,8 +22,8 @@ REMARKS = _lib.CSRC / "build" / "drt_kernels.remarks"
 BUDGET = {
     # headline (BASELINE configs[1..3]): AA frames, triangle-only scene, no stats
     "drt::path_persistent<true, false, 0, 6, 2>": (80, 2336, 6, 67),
-    # C4: in-order keyed-stream frames (DoF / glossy)
-    "drt::path_persistent<true, false, 1, 6, 2>": (80, 2416, 6, 106),
+    # C4: in-order keyed-stream frames (DoF / glossy); +48 B of scratch with the tail hand-over
+    "drt::path_persistent<true, false, 1, 6, 2>": (80, 2464, 6, 106),
     # Whitted point-light frames on mixed primitives (the shipped Whitted scenes on a BVH)
     "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 65),
     # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs)
