@@ -661,6 +661,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       P.F.seq_cap = cap;
       P.F.seq_slack = std::max(100, env_int("DRT_SEQ_SLACK", 100));
       P.F.seq_pop_min = std::min(64, std::max(1, env_int("DRT_SEQ_POP_MIN", 8)));
+      P.F.seq_backlog = (uint32_t)std::max(0, env_int("DRT_SEQ_BACKLOG", 0));
     }  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
   if (P.F.n_items) {

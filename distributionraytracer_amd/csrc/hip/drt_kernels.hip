@@ -1256,6 +1256,11 @@ struct FrameStack {
 // on itself) when the state does not fit the word or the slots are used up.
 __device__ __forceinline__ bool seq_donate(const FrameArgs& F, const Lane& L) {
   if (L.smp >= (1u << 12) || L.rk >= (1u << 20)) return false;
+  if (F.seq_backlog) {  // keep the pixel while this many handed-over pixels still wait for a lane
+    const unsigned long long pp = __hip_atomic_load((unsigned long long*)(F.work_counter + kSeqPush), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)pp - (uint32_t)(pp >> 32) >= F.seq_backlog) return false;
+  }
   const uint32_t idx = atomicAdd(F.work_counter + kSeqPush, 1u);
   if (idx >= F.seq_cap) return false;
   const unsigned long long v = (unsigned long long)L.item | ((unsigned long long)(L.smp | (L.rk << 12)) << 32);

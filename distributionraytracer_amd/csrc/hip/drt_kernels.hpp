@@ -117,6 +117,7 @@ struct FrameArgs {
   uint32_t seq_cap;            // continuation slots (one per resident lane bounds the pushes)
   int seq_slack;               // waves kept = ceil(unfinished pixels * seq_slack / 100 / 64)
   int seq_pop_min;             // a kept wave takes handed-over pixels once this many lanes are idle
+  uint32_t seq_backlog;        // a lane keeps its pixel while this many wait in the slots (0: no bound)
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

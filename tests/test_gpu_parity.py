@@ -534,7 +534,8 @@ def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, mo
     waves at sample boundaries once every pixel is claimed (FrameArgs::seq_cont).  A handed-over
     pixel goes on from the same sample and keyed-stream position, so the frame and every ray /
     traversal count equal the frame with the hand-over off (DRT_SEQ_DONATE=0), bit for bit, for
-    any number of waves kept (DRT_SEQ_SLACK), on the BVH and the Grid kernel, and with frames in
+    any number of waves kept (DRT_SEQ_SLACK) or pixels waiting (DRT_SEQ_BACKLOG), on the BVH and
+    the Grid kernel, and with frames in
     flight on several scratch slots.  The 1M-triangle scene makes the samples long enough for
     waves to hand pixels over mid-pixel."""
     import torch
@@ -550,8 +551,9 @@ def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, mo
     ref = renderer.render(seed=13, stats=True, **kw)
     rst = renderer.stats()
     monkeypatch.setenv("DRT_SEQ_DONATE", "1")
-    for slack in ("100", "150", "400"):
+    for slack, backlog in (("100", "0"), ("150", "0"), ("400", "0"), ("100", "64")):
         monkeypatch.setenv("DRT_SEQ_SLACK", slack)
+        monkeypatch.setenv("DRT_SEQ_BACKLOG", backlog)
         img = renderer.render(seed=13, stats=True, **kw)
         st = renderer.stats()
         np.testing.assert_array_equal(bits(img), bits(ref), err_msg=f"slack {slack}")
@@ -559,6 +561,7 @@ def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, mo
                   "closest_prims", "shadow_prims", "samples"):
             assert st[k] == rst[k], (slack, k)
     monkeypatch.delenv("DRT_SEQ_SLACK")
+    monkeypatch.delenv("DRT_SEQ_BACKLOG")
     streams = [torch.cuda.Stream() for _ in range(2)]
     outs = [torch.zeros((192, 192, 3), dtype=torch.float32, device="cuda") for _ in range(4)]
     for i in range(4):
