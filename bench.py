@@ -106,7 +106,29 @@ def cpu_baseline(args, tris, res, spp, seed, target_s, threads, ext):
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"rows {y0}-{y0 + rows - 1} of the {res}x{res}x{spp}spp frame ({rows * res * spp} samples, "
                       f"{rays} rays) in {dt:.1f} s; oracle BVH build {build_s:.1f} s",
-            "seconds": round(dt, 2)}
+            "seconds": round(dt, 2), **host_cpu_info(),
+            # the oracle against the reference itself, same scenes, measured in the build container
+            # (DESIGN.md §5): per thread the oracle is 1.2-1.3x the reference and it scales better
+            # (the reference opens a nested OpenMP region and allocates per pixel)
+            "calibration": {"oracle_over_reference_1_thread": {"1M_tris": 1.30, "100k_tris": 1.18},
+                            "oracle_over_reference_8_threads": {"1M_tris": 2.46, "100k_tris": 1.44},
+                            "source": "DESIGN.md §5 (512^2 x 1 spp BVH frames, 8-core container, BASELINE.md)"}}
+
+
+def host_cpu_info():
+    """The host's CPUs as this process sees them: nproc, the affinity set the oracle threads run
+    on, and the cgroup CPU quota (cpu.max) that may cap them below that."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        pass
+    return info
 
 
 def interval_union(starts, ends):
@@ -437,7 +459,9 @@ def main():
                             "shade": round(tot["cycles_shade"] / max(1.0, tot["wave_path_iters"]), 1)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        from oracle import oracle as O
+
+        threads = O.host_threads()  # every host core this process may run on (nproc stated in the line)
         try:
             out["cpu_baseline"] = cpu_baseline(args, tris, args.res, args.spp, args.seed, args.cpu_seconds, threads,
                                                ext)

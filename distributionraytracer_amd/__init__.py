@@ -120,6 +120,10 @@ class Scene:
         check(_lib.load().drt_scene_set_camera(self.h, _fp(_f32(eye)), _fp(_f32(at)), _fp(_f32(up)), fovy, hither,
                                                res_x, res_y, aperture, focal), what="set_camera")
 
+    def set_eye(self, eye):
+        """Camera::SetEye (camera.h:63-72): the interactive camera motion of main.cpp:530-533."""
+        check(_lib.load().drt_scene_set_eye(self.h, _fp(_f32(eye))), what="set_eye")
+
     def set_background(self, rgb):
         _lib.load().drt_scene_set_background(self.h, _fp(_f32(rgb)))
 
@@ -250,6 +254,17 @@ class Renderer:
     def upload(self, scene: Scene):
         check(_lib.load().drt_scene_upload(self.h, scene.h), self.h, "drt_scene_upload")
         self.scene = scene
+        return self
+
+    def set_camera(self, camera=None):
+        """drt_set_camera: the uploaded scene's camera alone (the per-frame SetEye of the interactive
+        renderer, main.cpp:530-533); `camera` is a Scene (its current camera) or a DrtCamera frame,
+        default the uploaded Scene.  Primitives and the accelerator stay resident."""
+        cam = self.scene if camera is None else camera
+        if isinstance(cam, Scene):
+            check(_lib.load().drt_scene_upload_camera(self.h, cam.h), self.h, "drt_scene_upload_camera")
+        else:
+            check(_lib.load().drt_set_camera(self.h, C.byref(cam)), self.h, "drt_set_camera")
         return self
 
     def frame_params(self, seed=1, max_depth=4, roughness=0.0, shard=0, n_shards=1, tile=16, stats=False,
@@ -402,18 +417,29 @@ class RendererGroup:
         self.scene = scene
         return self
 
-    def render(self, seed=1, max_depth=4, roughness=0.0, light_spp=1, progressive_frame=0, accum=None):
+    def set_camera(self, camera=None):
+        """drt_group_set_camera on every device (see Renderer.set_camera)."""
+        cam = self.scene if camera is None else camera
+        if isinstance(cam, Scene):
+            self._check(_lib.load().drt_group_scene_upload_camera(self.h, cam.h), "drt_group_scene_upload_camera")
+        else:
+            self._check(_lib.load().drt_group_set_camera(self.h, C.byref(cam)), "drt_group_set_camera")
+        return self
+
+    def render(self, seed=1, max_depth=4, roughness=0.0, light_spp=1, progressive_frame=0, accum=None, slot=0):
         info = self.scene.info()
         out = accum if accum is not None else np.zeros((info.res_y, info.res_x, 3), np.float32)
         p = DrtFrameParams()
         p.seed, p.max_depth, p.roughness, p.light_spp, p.progressive_frame = seed, max_depth, roughness, light_spp, \
             progressive_frame
+        p.slot = slot
         self._check(_lib.load().drt_group_render(self.h, C.byref(p), _fp(out)), "drt_group_render")
         return out
 
-    def render_device(self, d_frame_ptr, seed=1, max_depth=4, roughness=0.0, light_spp=1, stream=None):
+    def render_device(self, d_frame_ptr, seed=1, max_depth=4, roughness=0.0, light_spp=1, stream=None, slot=0):
         p = DrtFrameParams()
         p.seed, p.max_depth, p.roughness, p.light_spp = seed, max_depth, roughness, light_spp
+        p.slot = slot
         self._check(_lib.load().drt_group_render_device(self.h, C.byref(p), C.c_void_p(d_frame_ptr),
                                                         C.c_void_p(stream or 0)), "drt_group_render_device")
 

@@ -51,10 +51,12 @@ class DrtFrameStats(C.Structure):
                                           "samples")] + [("render_ms", C.c_double), ("kernel_ms", C.c_double)] + \
         [(n, C.c_uint64) for n in ("wave_node_iters", "wave_path_iters", "lane_path_iters", "cycles_refill",
                                    "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
-                                   "wave_leaf_iters", "cycles_leaf")]
+                                   "wave_leaf_iters", "cycles_leaf", "seq_pushed", "seq_popped")] + \
+        [("seq_handover", C.c_int32), ("reserved", C.c_int32 * 3)]
 
     def as_dict(self):
-        return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_}
+        return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_
+                if n != "reserved"}
 
 
 class DrtFramePlan(C.Structure):
@@ -101,6 +103,7 @@ SIGNATURES = {
     "drt_destroy": (None, [_vp]),
     "drt_last_error": (C.c_char_p, [_vp]),
     "drt_upload_scene": (C.c_int, [_vp, C.POINTER(DrtSceneDesc)]),
+    "drt_set_camera": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
     "drt_upload_bvh": (C.c_int, [_vp, _vp, C.c_uint32, _u32, C.c_uint32]),
     "drt_upload_grid": (C.c_int, [_vp, _i32, _f, _f, _i64, _i32, C.c_int64]),
     "drt_render": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _f]),
@@ -126,6 +129,7 @@ SIGNATURES = {
     "drt_group_render": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _f]),
     "drt_group_render_device": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _vp, _vp]),
     "drt_group_synchronize": (C.c_int, [_vp]),
+    "drt_group_set_camera": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
     # drt_host.h
     "drt_group_scene_upload": (C.c_int, [_vp, _vp]),
     "drt_scene_new": (_vp, []),
@@ -154,6 +158,9 @@ SIGNATURES = {
     "drt_scene_grid_export": (C.c_int, [_vp, _i64, _i32]),
     "drt_scene_camera_frame": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
     "drt_scene_upload": (C.c_int, [_vp, _vp]),
+    "drt_scene_set_eye": (C.c_int, [_vp, _f]),
+    "drt_scene_upload_camera": (C.c_int, [_vp, _vp]),
+    "drt_group_scene_upload_camera": (C.c_int, [_vp, _vp]),
     "drt_set_image_decoder": (C.c_int, [_vp, _vp]),
     "drt_scene_load_skybox": (C.c_int, [_vp, C.c_char_p]),
     "drt_scene_trace_cpu": (C.c_int, [_vp, C.c_int, _f, C.c_int64, _f, _f, _i32, _u8]),

@@ -119,7 +119,17 @@ struct drt_ctx {
   // shuffle of that slot rewrites the permutation it reads).
   hipStream_t aux[DRT_FRAME_SLOTS] = {};
   hipEvent_t ev_shuf[DRT_FRAME_SLOTS] = {}, ev_path[DRT_FRAME_SLOTS] = {}, ev_red[DRT_FRAME_SLOTS] = {};
+  // ev_path[slot] is recorded after EVERY path kernel of the slot (aux frame or not), so an aux
+  // shuffle that rewrites the slot's permutation always waits for the last kernel reading it
   bool path_issued[DRT_FRAME_SLOTS] = {};
+  // The slot's last frame: its ring entry (frame number) and the stream it ran on.  A frame on the
+  // same slot from another stream waits for that frame's end event first (its samples, counters
+  // and permutation are the slot's scratch).
+  uint64_t slot_frame[DRT_FRAME_SLOTS] = {};
+  hipStream_t slot_stream[DRT_FRAME_SLOTS] = {};
+  bool slot_used[DRT_FRAME_SLOTS] = {};
+  // MODE_SEQ hand-over of the slot's last frame (drt_frame_stats.seq_handover)
+  bool slot_handover[DRT_FRAME_SLOTS] = {};
   // The auxiliary streams cost each frame ~0.17 ms of cross-stream event latency, which only
   // pays for itself on long frames: they are used once a completed frame's path kernel took
   // >= kAuxMinMs (DRT_AUX_STREAMS=0 / 1 forces them off / on).  -1 = no completed frame yet.
@@ -300,6 +310,16 @@ int drt_upload_scene(drt_ctx* c, const drt_scene_desc* s) {
   c->prims_scene = std::move(prims);
   c->tri_only = tri_only;
   c->has_scene = true;
+  return DRT_OK;
+}
+
+int drt_set_camera(drt_ctx* c, const drt_camera* k) {
+  if (!c || !k) return DRT_E_INVALID;
+  if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "set the camera of an uploaded scene");
+  if (k->res_x <= 0 || k->res_y <= 0) DRT_FAIL(c, DRT_E_INVALID, "camera resolution must be positive");
+  // the frame reaches the kernels by value (SceneArgs, copied at launch): frames already issued
+  // keep the camera they were launched with
+  c->cam = *k;
   return DRT_OK;
 }
 
@@ -605,6 +625,29 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   DevBuf& d_samples = c->d_samples_s[slot];
   DevBuf& d_stats = c->d_stats_s[slot];
   DevBuf& d_counter = c->d_counter_s[slot];
+  // The slot's scratch is reused: a frame from another stream than the slot's last frame waits for
+  // that frame to end (on the device).  Frames of one stream are ordered by the stream itself.
+  if (c->slot_used[slot] && c->slot_stream[slot] != st && c->frames - c->slot_frame[slot] < drt_ctx::kRing)
+    DRT_HIP(c, hipStreamWaitEvent(st, c->ring[3 * (c->slot_frame[slot] % drt_ctx::kRing) + 2], 0));
+  // MODE_SEQ tail hand-over (DRT_SEQ_DONATE: 0 off, 1 on, default auto).  It frees whole blocks
+  // at the frame's tail for the NEXT frame's blocks, but makes a frame alone slower (a handed-over
+  // pixel waits for a lane of a kept wave: C4 820-828 -> 853-902 ms).  Auto turns it
+  // on when another frame of this context is still in flight on another stream at issue time —
+  // the pipelined case, where a frame follows on the freed CUs.
+  bool handover = false;
+  c->slot_handover[slot] = false;
+  {
+    const int dm = env_int("DRT_SEQ_DONATE", -1);
+    if (dm >= 0) {
+      handover = dm != 0;
+    } else {
+      for (int k = 0; k < DRT_FRAME_SLOTS && !handover; k++) {
+        if (k == slot || !c->slot_used[k] || c->slot_stream[k] == st) continue;
+        if (c->frames - c->slot_frame[k] >= drt_ctx::kRing) continue;
+        handover = hipEventQuery(c->ring[3 * (c->slot_frame[k] % drt_ctx::kRing) + 2]) == hipErrorNotReady;
+      }
+    }
+  }
   c->stats_slot = slot;
   DRT_HIP(c, d_samples.ensure(sizeof(float4) * std::max<uint64_t>(1, P.n_slots)));
   DRT_HIP(c, d_stats.ensure(sizeof(unsigned long long) * ST_COUNT));
@@ -626,6 +669,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   if (P.persistent && shuffled && P.F.spp >= 2 && P.F.spp <= 256 && P.F.n_items && env_int("DRT_PERM", 1)) {
     DevBuf& d_perm = c->d_perm_s[slot];
     DRT_HIP(c, d_perm.ensure((size_t)P.F.n_my_tiles * P.F.tile * P.F.tile * P.F.spp));
+    // the slot's previous path kernel reads the permutation this shuffle rewrites (on the caller's
+    // stream that order is the stream's own, or the slot wait above)
     if (use_aux && c->path_issued[slot]) DRT_HIP(c, hipStreamWaitEvent(ax, c->ev_path[slot], 0));
     launch_shuffle(P.F, c->cam.res_x, c->cam.res_y, d_perm.as<uint8_t>(), ax);
     P.F.perm = d_perm.as<uint8_t>();
@@ -636,6 +681,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     }
   }
   hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
+  c->slot_frame[slot] = c->frames;
+  c->slot_stream[slot] = st;
+  c->slot_used[slot] = true;
   c->frames++;
   DRT_HIP(c, hipEventRecord(ev[0], st));
   const bool persistent = P.persistent;
@@ -649,9 +697,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     P.F.waves = env_int("DRT_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 6);
     P.F.grid_pairs = std::max(1, env_int("DRT_GRID_PAIRS", 3));  // >= 1: a lane must make progress
     P.F.grid_walk = std::max(0, env_int("DRT_GRID_WALK", 5));
-    // MODE_SEQ tail hand-over (DRT_SEQ_DONATE=0: off; DRT_SEQ_SLACK: percent of the waves the
-    // unfinished pixels need that stay, >= 100)
-    if (P.F.mode == MODE_SEQ && env_int("DRT_SEQ_DONATE", 1)) {
+    // MODE_SEQ tail hand-over (`handover` above)
+    if (P.F.mode == MODE_SEQ && handover) {
+      c->slot_handover[slot] = true;
       if (!c->cus) DRT_HIP(c, hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
       const uint32_t cap = (uint32_t)std::max(1, c->cus) * 2048u;  // 32 waves of 64 lanes per CU at most
       DevBuf& d_cont = c->d_cont_s[slot];
@@ -659,8 +707,12 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       DRT_HIP(c, hipMemsetAsync(d_cont.p, 0, sizeof(unsigned long long) * cap, st));
       P.F.seq_cont = d_cont.as<unsigned long long>();
       P.F.seq_cap = cap;
-      P.F.seq_slack = std::max(100, env_int("DRT_SEQ_SLACK", 100));
-      P.F.seq_pop_min = std::min(64, std::max(1, env_int("DRT_SEQ_POP_MIN", 8)));
+      // Kept waves: exactly what the unfinished pixels need.  More (slack above 100 %) and a higher
+      // idle-lane threshold for pops measured 1.5-4x slower frames (contention on the one push/pop
+      // line): the slack is fixed and the threshold clamped to the range that measured
+      // sane.
+      P.F.seq_slack = 100;
+      P.F.seq_pop_min = std::min(32, std::max(1, env_int("DRT_SEQ_POP_MIN", 8)));
       P.F.seq_backlog = (uint32_t)std::max(0, env_int("DRT_SEQ_BACKLOG", 0));
     }  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
@@ -670,10 +722,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   }
   DRT_HIP(c, hipGetLastError());
   DRT_HIP(c, hipEventRecord(ev[1], st));
-  if (use_aux) {
-    DRT_HIP(c, hipEventRecord(c->ev_path[slot], st));
-    c->path_issued[slot] = true;
-  }
+  DRT_HIP(c, hipEventRecord(c->ev_path[slot], st));  // every frame: the slot's last path kernel
+  c->path_issued[slot] = true;
   if (P.F.n_my_tiles) {
     if (use_aux) DRT_HIP(c, hipStreamWaitEvent(ax, c->ev_path[slot], 0));
     launch_reduce(P.R, ax);
@@ -829,6 +879,14 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.stack_spills = s[ST_PUSH_SPILL];
       c->last.wave_leaf_iters = s[ST_WAVE_LEAF_ITERS];
       c->last.cycles_leaf = s[ST_CYC_LEAF];
+    }
+    c->last.seq_handover = c->slot_handover[c->stats_slot] ? 1 : 0;
+    if (c->last.seq_handover) {  // push / pop counts of the frame's continuation slots
+      uint32_t pp[2] = {0, 0};
+      DRT_HIP(c, hipMemcpy(pp, c->d_counter_s[c->stats_slot].as<unsigned int>() + kSeqPush, sizeof(pp),
+                           hipMemcpyDeviceToHost));
+      c->last.seq_pushed = pp[0];
+      c->last.seq_popped = pp[1];
     }
   }
   *out = c->last;

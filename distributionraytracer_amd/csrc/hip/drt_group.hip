@@ -68,8 +68,13 @@ struct drt_group {
   std::vector<drt_ctx*> ctx;
   std::vector<hipStream_t> stream;
   std::vector<ncclComm_t> comm;     // one per device
-  std::vector<float*> shard, gathered;  // per device: its shard buffer, the all-gathered shards
-  std::vector<size_t> shard_floats;    // current allocation (floats per shard)
+  // per frame slot (drt_frame_params.slot) and device: its shard buffer, the all-gathered shards.
+  // Frames on different slots own different buffers; a frame on a slot whose last frame ran on
+  // another stream0 waits (on device 0) for that frame's reassembly, which reads them.
+  std::vector<float*> shard[DRT_FRAME_SLOTS], gathered[DRT_FRAME_SLOTS];
+  std::vector<size_t> shard_floats[DRT_FRAME_SLOTS];  // current allocation (floats per shard)
+  hipEvent_t slot_done[DRT_FRAME_SLOTS] = {};          // device 0: after the slot's last unshard
+  hipStream_t slot_stream[DRT_FRAME_SLOTS] = {};
   float* d_frame = nullptr;            // device 0: reassembled frame for drt_group_render
   size_t frame_floats = 0;
   std::string err;
@@ -102,8 +107,11 @@ void drt_group_destroy(drt_group* g) {
       if (c) rccl().commDestroy(c);
   for (int r = 0; r < g->n; r++) {
     (void)hipSetDevice(g->dev[r]);
-    if (r < (int)g->shard.size() && g->shard[r]) (void)hipFree(g->shard[r]);
-    if (r < (int)g->gathered.size() && g->gathered[r]) (void)hipFree(g->gathered[r]);
+    for (int k = 0; k < DRT_FRAME_SLOTS; k++) {
+      if (r < (int)g->shard[k].size() && g->shard[k][r]) (void)hipFree(g->shard[k][r]);
+      if (r < (int)g->gathered[k].size() && g->gathered[k][r]) (void)hipFree(g->gathered[k][r]);
+      if (r == 0 && g->slot_done[k]) (void)hipEventDestroy(g->slot_done[k]);
+    }
     if (r < (int)g->stream.size() && g->stream[r]) (void)hipStreamDestroy(g->stream[r]);
     if (r < (int)g->ctx.size() && g->ctx[r]) drt_destroy(g->ctx[r]);
   }
@@ -131,9 +139,11 @@ int drt_group_create(drt_group** out, int n_devices, const int32_t* devices) {
   g->dev = dev;
   g->ctx.assign(n_devices, nullptr);
   g->stream.assign(n_devices, nullptr);
-  g->shard.assign(n_devices, nullptr);
-  g->gathered.assign(n_devices, nullptr);
-  g->shard_floats.assign(n_devices, 0);
+  for (int k = 0; k < DRT_FRAME_SLOTS; k++) {
+    g->shard[k].assign(n_devices, nullptr);
+    g->gathered[k].assign(n_devices, nullptr);
+    g->shard_floats[k].assign(n_devices, 0);
+  }
   for (int r = 0; r < n_devices; r++) {
     drt_options opt{};
     opt.device = dev[r];
@@ -147,6 +157,12 @@ int drt_group_create(drt_group** out, int n_devices, const int32_t* devices) {
       return DRT_E_HIP;
     }
   }
+  (void)hipSetDevice(dev[0]);
+  for (int k = 0; k < DRT_FRAME_SLOTS; k++)
+    if (hipEventCreateWithFlags(&g->slot_done[k], hipEventDisableTiming) != hipSuccess) {
+      drt_group_destroy(g);
+      return DRT_E_HIP;
+    }
   {  // every group, one device included, runs the same shard -> all-gather -> unshard path
     const Rccl& R = rccl();
     if (!R.ok) {
@@ -169,6 +185,15 @@ const char* drt_group_last_error(const drt_group* g) { return g ? g->err.c_str()
 int drt_group_size(const drt_group* g) { return g ? g->n : DRT_E_INVALID; }
 
 drt_ctx* drt_group_ctx(drt_group* g, int rank) { return (g && rank >= 0 && rank < g->n) ? g->ctx[rank] : nullptr; }
+
+int drt_group_set_camera(drt_group* g, const drt_camera* camera) {
+  if (!g || !camera) return DRT_E_INVALID;
+  for (int r = 0; r < g->n; r++) {
+    const int rc = drt_set_camera(g->ctx[r], camera);
+    if (rc) G_FAIL(g, rc, "device %d: %s", g->dev[r], drt_last_error(g->ctx[r]));
+  }
+  return DRT_OK;
+}
 
 int drt_group_render_device(drt_group* g, const drt_frame_params* params, float* d_frame, void* stream0) {
   if (!g || !params || !d_frame) return DRT_E_INVALID;
@@ -199,26 +224,36 @@ int drt_group_render_device(drt_group* g, const drt_frame_params* params, float*
     else if (f != floats) G_FAIL(g, DRT_E_STATE, "devices hold different scenes (shard sizes %lld vs %lld)",
                                  (long long)f, (long long)floats);
   }
+  const int slot = params->slot;
+  if (slot < 0 || slot >= DRT_FRAME_SLOTS) G_FAIL(g, DRT_E_INVALID, "frame slot out of range");
+  std::vector<float*>& shard = g->shard[slot];
+  std::vector<float*>& gathered = g->gathered[slot];
+  // the slot's buffers: the last frame on this slot may still be gathering / reassembling them on
+  // another stream0 (devices r > 0 always use the group's own stream, which orders them)
+  G_HIP(g, hipSetDevice(g->dev[0]));
+  if (g->slot_stream[slot] && g->slot_stream[slot] != s0) G_HIP(g, hipStreamWaitEvent(s0, g->slot_done[slot], 0));
   // the frame's shards, each device on its own stream (device 0 on the caller's stream)
   for (int r = 0; r < g->n; r++) {
     G_HIP(g, hipSetDevice(g->dev[r]));
-    if (g->shard_floats[r] < (size_t)floats) {
-      if (g->shard[r]) G_HIP(g, hipFree(g->shard[r]));
-      if (g->gathered[r]) G_HIP(g, hipFree(g->gathered[r]));
-      g->shard[r] = g->gathered[r] = nullptr;
-      g->shard_floats[r] = 0;
-      G_HIP(g, hipMalloc(&g->shard[r], sizeof(float) * (size_t)floats));
-      G_HIP(g, hipMalloc(&g->gathered[r], sizeof(float) * (size_t)floats * g->n));
-      g->shard_floats[r] = (size_t)floats;
+    if (g->shard_floats[slot][r] < (size_t)floats) {
+      // regrowing: the slot's previous frame must be done with the old buffers on this device
+      G_HIP(g, hipStreamSynchronize(r == 0 ? s0 : g->stream[r]));
+      if (shard[r]) G_HIP(g, hipFree(shard[r]));
+      if (gathered[r]) G_HIP(g, hipFree(gathered[r]));
+      shard[r] = gathered[r] = nullptr;
+      g->shard_floats[slot][r] = 0;
+      G_HIP(g, hipMalloc(&shard[r], sizeof(float) * (size_t)floats));
+      G_HIP(g, hipMalloc(&gathered[r], sizeof(float) * (size_t)floats * g->n));
+      g->shard_floats[slot][r] = (size_t)floats;
     }
-    const int rc = drt_render_device(g->ctx[r], &p[r], g->shard[r], r == 0 ? s0 : g->stream[r]);
+    const int rc = drt_render_device(g->ctx[r], &p[r], shard[r], r == 0 ? s0 : g->stream[r]);
     if (rc) G_FAIL(g, rc, "device %d: %s", g->dev[r], drt_last_error(g->ctx[r]));
   }
   // one all-gather of the shard buffers (each stream orders it after its device's shard)
   const Rccl& R = rccl();
   if (R.groupStart() != ncclSuccess) G_FAIL(g, DRT_E_HIP, "ncclGroupStart failed");
   for (int r = 0; r < g->n; r++) {
-    const ncclResult_t e = R.allGather(g->shard[r], g->gathered[r], (size_t)floats, ncclFloat, g->comm[r],
+    const ncclResult_t e = R.allGather(shard[r], gathered[r], (size_t)floats, ncclFloat, g->comm[r],
                                        r == 0 ? s0 : g->stream[r]);
     if (e != ncclSuccess) {
       R.groupEnd();
@@ -229,8 +264,10 @@ int drt_group_render_device(drt_group* g, const drt_frame_params* params, float*
   if (e != ncclSuccess) G_FAIL(g, DRT_E_HIP, "ncclGroupEnd: %s", R.errorString(e));
   // device 0 reassembles the frame
   G_HIP(g, hipSetDevice(g->dev[0]));
-  const int rc = drt_unshard_device(g->ctx[0], &p[0], g->gathered[0], d_frame, s0);
+  const int rc = drt_unshard_device(g->ctx[0], &p[0], gathered[0], d_frame, s0);
   if (rc) G_FAIL(g, rc, "unshard: %s", drt_last_error(g->ctx[0]));
+  G_HIP(g, hipEventRecord(g->slot_done[slot], s0));
+  g->slot_stream[slot] = s0;
   return DRT_OK;
 }
 

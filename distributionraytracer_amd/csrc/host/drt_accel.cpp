@@ -303,6 +303,16 @@ int upload_scene(drt_ctx* ctx, const Scene& scene, const BVH* bvh, const Grid* g
 
 int render_scene(drt_ctx* ctx, const drt_frame_params& p, float* colors) { return drt_render(ctx, &p, colors); }
 
+int set_camera(drt_ctx* ctx, const Camera& camera) {
+  const drt_camera k = camera.frame();
+  return drt_set_camera(ctx, &k);
+}
+
+int set_camera(drt_group* g, const Camera& camera) {
+  const drt_camera k = camera.frame();
+  return drt_group_set_camera(g, &k);
+}
+
 int upload_scene(drt_group* g, const Scene& scene, const BVH* bvh, const Grid* grid) {
   const int n = drt_group_size(g);
   if (n <= 0) return DRT_E_INVALID;

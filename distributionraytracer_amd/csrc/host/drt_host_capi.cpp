@@ -187,6 +187,28 @@ int drt_scene_camera_frame(const drt_scene* s, drt_camera* out) {
   return DRT_OK;
 }
 
+int drt_scene_set_eye(drt_scene* s, const float eye[3]) {
+  if (!s || !eye) return DRT_E_INVALID;
+  Camera* c = s->scene.GetCamera();
+  if (!c) return DRT_E_STATE;
+  c->SetEye(Vector(eye[0], eye[1], eye[2]));
+  return DRT_OK;
+}
+
+int drt_scene_upload_camera(drt_ctx* ctx, const drt_scene* s) {
+  if (!ctx || !s) return DRT_E_INVALID;
+  const Camera* c = s->scene.GetCamera();
+  if (!c) return DRT_E_STATE;
+  return set_camera(ctx, *c);
+}
+
+int drt_group_scene_upload_camera(drt_group* g, const drt_scene* s) {
+  if (!g || !s) return DRT_E_INVALID;
+  const Camera* c = s->scene.GetCamera();
+  if (!c) return DRT_E_STATE;
+  return set_camera(g, *c);
+}
+
 int drt_scene_upload(drt_ctx* ctx, drt_scene* s) {
   if (!ctx || !s) return DRT_E_INVALID;
   if (!s->scene.GetCamera()) return DRT_E_STATE;

@@ -8,6 +8,8 @@
  *
  *   drt_upload_scene   <- Scene / Camera / Light / Material / Object state read by
  *                         rayTracing() (scene.h:24-231, camera.h:12-101)
+ *   drt_set_camera     <- Camera::SetEye (camera.h:63-72), called by renderScene() every frame
+ *                         in draw mode (main.cpp:530-533): the camera alone, scene resident
  *   drt_upload_bvh     <- BVH::Build result (rayAccelerator.h:87-94, bvh.cpp:27-227)
  *   drt_upload_grid    <- Grid::Build result (rayAccelerator.h:12-37, grid.cpp:30-97)
  *   drt_trace_closest  <- BVH::Traverse(Ray&, Object**, HitRecord&)  (bvh.cpp:231-314)
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DRT_ABI_VERSION 1
+#define DRT_ABI_VERSION 2
 #define DRT_FRAME_SLOTS 4 /* drt_frame_params.slot: 0 .. DRT_FRAME_SLOTS-1 */
 
 typedef enum {
@@ -145,7 +147,9 @@ typedef struct {
                           leaves the output untouched (main.cpp:537)                     */
   int32_t slot;        /* frame scratch slot, 0 .. DRT_FRAME_SLOTS-1: frames on different
                           slots of one context may run concurrently on different streams
-                          (pipelining); other values are DRT_E_INVALID                    */
+                          (pipelining); a frame on a slot whose previous frame ran on another
+                          stream waits for that frame on the device; other values are
+                          DRT_E_INVALID                                                    */
   int32_t reserved[2];
 } drt_frame_params;
 
@@ -162,6 +166,11 @@ typedef struct {
   uint64_t cycles_refill, cycles_node, cycles_shade; /* persistent kernel: s_memtime cycles */
   uint64_t stack_pushes, stack_spills;   /* traversal-stack pushes / those beyond the LDS part */
   uint64_t wave_leaf_iters, cycles_leaf; /* node-loop iterations that ran the leaf block / its cycles */
+  /* in-order keyed-stream frames (DoF / glossy): pixels handed between waves at the frame's tail
+   * and taken up again (0 when the hand-over was off for the frame); filled for every frame */
+  uint64_t seq_pushed, seq_popped;
+  int32_t seq_handover;                   /* the hand-over was on for the frame                  */
+  int32_t reserved[3];
 } drt_frame_stats;
 
 int drt_create(drt_ctx** out, const drt_options* opt);
@@ -170,6 +179,11 @@ const char* drt_last_error(const drt_ctx* ctx);
 int drt_abi_version(void);
 
 int drt_upload_scene(drt_ctx* ctx, const drt_scene_desc* scene);
+/* Replace the camera of the resident scene (Camera::SetEye, camera.h:63-72; the interactive
+ * renderer calls it every frame, main.cpp:530-533).  Primitives, lights, materials, skybox and
+ * the BVH / grid stay resident: nothing is re-packed or copied.  The next frame issued uses the
+ * new camera; frames already issued keep theirs.  DRT_E_STATE without a scene. */
+int drt_set_camera(drt_ctx* ctx, const drt_camera* camera);
 int drt_upload_bvh(drt_ctx* ctx, const drt_bvh_node* nodes, uint32_t n_nodes, const uint32_t* object_order,
                    uint32_t n_objects);
 int drt_upload_grid(drt_ctx* ctx, const int32_t dims[3], const float bmin[3], const float bmax[3],
@@ -258,8 +272,13 @@ drt_ctx* drt_group_ctx(drt_group* g, int rank);
  * n_shards 0 or 1 (the group deals the tiles). */
 int drt_group_render(drt_group* g, const drt_frame_params* params, float* rgb_out);
 /* Whole frame into DEVICE memory on device 0 (d_frame: RES_Y*RES_X*3 floats), asynchronous:
- * device 0's work on `stream0` (NULL = the group's), the other devices' on the group's streams. */
+ * device 0's work on `stream0` (NULL = the group's), the other devices' on the group's streams.
+ * Shard and gather buffers belong to params->slot: frames on different slots do not share them,
+ * and a frame on a slot whose last frame ran on another stream0 waits for that frame's reassembly
+ * (on the device). */
 int drt_group_render_device(drt_group* g, const drt_frame_params* params, float* d_frame, void* stream0);
+/* drt_set_camera on every device of the group. */
+int drt_group_set_camera(drt_group* g, const drt_camera* camera);
 /* Wait for every device's stream. */
 int drt_group_synchronize(drt_group* g);
 

@@ -73,10 +73,18 @@ int drt_scene_bvh_export(const drt_scene* s, float* boxes, uint32_t* leaf, uint3
 int drt_scene_grid_export_dims(const drt_scene* s, int32_t dims[3], float bmin[3], float bmax[3], int64_t* n_refs);
 int drt_scene_grid_export(const drt_scene* s, int64_t* cell_start, int32_t* cell_objs);
 int drt_scene_camera_frame(const drt_scene* s, drt_camera* out);
+/* Camera::SetEye (camera.h:63-72): new eye, frame u/v/n and plane distance recomputed; the view
+ * window (w, h) and aperture keep their construction values, as in the reference.  DRT_E_STATE
+ * without a camera. */
+int drt_scene_set_eye(drt_scene* s, const float eye[3]);
 
 int drt_scene_upload(drt_ctx* ctx, drt_scene* s);
 /* drt_scene_upload to every device of a group (include/drt.h, drt_group_*). */
 int drt_group_scene_upload(drt_group* g, drt_scene* s);
+/* The scene's current camera frame to a context / every device of a group (drt_set_camera): the
+ * per-frame camera of the interactive renderer (main.cpp:530-533) with the scene resident. */
+int drt_scene_upload_camera(drt_ctx* ctx, const drt_scene* s);
+int drt_group_scene_upload_camera(drt_group* g, const drt_scene* s);
 
 /* ---- skybox faces from files (Scene::LoadSkybox, scene.cpp:329-378) ---- */
 /* A decoder for <dir>/<face>.jpg: fills *w, *h, *bpp (3 or 4) and *pixels (malloc'd, rows

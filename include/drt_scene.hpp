@@ -404,6 +404,10 @@ class Grid {
 // bottom) on the GPU.  Return drt_status codes.
 int upload_scene(drt_ctx* ctx, const Scene& scene, const BVH* bvh, const Grid* grid);
 int render_scene(drt_ctx* ctx, const drt_frame_params& params, float* colors);
+// The per-frame camera of the interactive renderer (main.cpp:530-533: SetEye, then renderScene):
+// the camera's current frame replaces the context's (drt_set_camera); the scene stays resident.
+int set_camera(drt_ctx* ctx, const Camera& camera);
+int set_camera(drt_group* group, const Camera& camera);
 // The same over several GPUs (include/drt.h, drt_group_*): the scene on every device, each frame
 // tile-sharded, all-gathered over RCCL and reassembled on device 0.
 int upload_scene(drt_group* group, const Scene& scene, const BVH* bvh, const Grid* grid);

@@ -274,6 +274,15 @@ struct Camera {  // camera.h:12-101
     w = ((float)res_x / res_y) * h;
     aperture = ap_ratio * (w / res_x);
   }
+  void set_eye(V3 from) {  // camera.h:63-72: frame and plane distance only; w, h, aperture stay
+    eye = from;
+    n = sub(eye, at);
+    plane_dist = length(n);
+    n = dvf(n, plane_dist);
+    u = cross(up, n);
+    u = dvf(u, length(u));
+    v = cross(n, u);
+  }
   Ray primary(V3 ps) const {  // camera.h:74-83
     float a = (float)((double)(ps.x / res_x) - 0.5);
     float b = (float)((double)(ps.y / res_y) - 0.5);
@@ -1275,6 +1284,12 @@ int orc_aabb_hit(const float* boxes, const float* rays, int n, uint8_t* hit, flo
     t[i] = tt;
     inside[i] = aabb_inside(b, r.o) ? 1 : 0;
   }
+  return 0;
+}
+
+int orc_scene_set_eye(orc_scene* s, const float eye[3]) {  // Camera::SetEye (camera.h:63-72)
+  if (!s->has_cam) return -1;
+  s->cam.set_eye(v3p(eye));
   return 0;
 }
 

@@ -116,6 +116,7 @@ int orc_ray_color(orc_scene*, const float* rays, const float* light_samples, int
 int orc_object_bbox(const orc_scene*, int obj, float out[6]);
 int orc_aabb_hit(const float* boxes, const float* rays, int n, uint8_t* hit, float* t, uint8_t* inside);
 int orc_camera_frame(const orc_scene*, float* frame13); /* plane_dist, aperture, w, h, u, v, n */
+int orc_scene_set_eye(orc_scene*, const float eye[3]);  /* Camera::SetEye, camera.h:63-72 */
 int orc_light_points(const orc_scene*, int light, const float* samples /* n x 3 */, int n, float* out);
 int orc_vector_ops(const float* a, const float* b, int n, float* nrm, float* len, float* crs, float* dotv);
 int orc_color_ops(const float* c, int n, float* clamped, float* ex, uint8_t* u8);

@@ -103,6 +103,7 @@ def lib():
         L.orc_ray_color.argtypes = [vp, _f, _f, C.c_int, C.c_int, C.c_float, C.c_uint32, C.c_uint32, _f]
         L.orc_aabb_hit.argtypes = [_f, _f, C.c_int, _u8, _f, _u8]
         L.orc_camera_frame.argtypes = [vp, _f]
+        L.orc_scene_set_eye.argtypes = [vp, _f]
         L.orc_light_points.argtypes = [vp, C.c_int, _f, C.c_int, _f]
         L.orc_vector_ops.argtypes = [_f, _f, C.c_int, _f, _f, _f, _f]
         L.orc_color_ops.argtypes = [_f, C.c_int, _f, _f, _u8]
@@ -194,6 +195,11 @@ class Scene:
     def set_camera(self, eye, at, up, fovy, hither, res_x, res_y, aperture=0.0, focal=1.0):
         lib().orc_scene_set_camera(self.h, fp(f32(eye)), fp(f32(at)), fp(f32(up)), fovy, hither, res_x, res_y,
                                    aperture, focal)
+
+    def set_eye(self, eye):
+        """Camera::SetEye (camera.h:63-72)."""
+        if lib().orc_scene_set_eye(self.h, fp(f32(eye))) != 0:
+            raise RuntimeError("set_eye: scene has no camera")
 
     def set_background(self, rgb):
         lib().orc_scene_set_background(self.h, fp(f32(rgb)))
@@ -334,6 +340,15 @@ class Scene:
         if rc:
             raise RuntimeError(f"orc_render failed ({rc})")
         return out, st.as_dict()
+
+
+def host_threads():
+    """Every host core this process may run on (sched_getaffinity): the CPU baselines and the
+    full-size parity checks run the oracle on all of them, whatever OMP_NUM_THREADS says."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return max(1, os.cpu_count() or 1)
 
 
 def keyed_rand(seed, pixel, k):

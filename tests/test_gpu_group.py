@@ -101,3 +101,41 @@ def test_cpp_caller_renders_group_frame(drt, tmp_path):
     mine = r.render(seed=11)
     r.close()
     np.testing.assert_array_equal(img.view(np.uint32), mine.view(np.uint32))
+
+
+def test_c5_workload_sharded_and_grouped_equal_whole_frame(drt):
+    """BASELINE config C5 on one GPU: the C4 workload (1M triangles + floor, 1024^2, 64 spp, DoF
+    aperture 8 focal 1, depth 8, roughness 0.1) split as the 8-GPU run splits it — eight
+    interleaved 16x16-tile shards, each rendered into its own shard-compact buffer, reassembled by
+    drt_unshard_device — and through a RendererGroup over every device of the box (shard ->
+    RCCL all-gather -> unshard).  Both equal the whole frame bit for bit (the loop being split is
+    main.cpp:603-721; the whole frame is checked against the oracle by
+    test_full_size_config_matches_oracle[C4...])."""
+    import torch
+
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(1_000_000), 1024, 64, aperture=8.0, focal=1.0)
+    s.build()
+    kw = dict(roughness=0.1, max_depth=8)
+    r = drt.Renderer(0)
+    r.upload(s)
+    whole = r.render(seed=7, **kw)
+    p0 = r.frame_params(seed=7, shard=0, n_shards=8, **kw)
+    tiles, floats = r.shard_layout(p0)
+    assert tiles * 8 >= (1024 // 16) ** 2
+    bufs = torch.zeros((8, floats), dtype=torch.float32, device="cuda")
+    for k in range(8):
+        r.render_device(r.frame_params(seed=7, shard=k, n_shards=8, **kw), bufs[k].data_ptr())
+    frame = torch.zeros((1024, 1024, 3), dtype=torch.float32, device="cuda")
+    r.unshard_device(p0, bufs.data_ptr(), frame.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(frame.cpu().numpy().view(np.uint32), whole.view(np.uint32))
+    r.close()
+    del bufs, frame
+    g = drt.RendererGroup(range(n_devices()))
+    g.upload(s)
+    gf = g.render(seed=7, **kw)
+    g.close()
+    np.testing.assert_array_equal(gf.view(np.uint32), whole.view(np.uint32))

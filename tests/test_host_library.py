@@ -48,7 +48,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in sorted(names) if not hasattr(L, n)]
     assert not missing, missing
     assert set(names) <= set(_lib.SIGNATURES), sorted(set(names) - set(_lib.SIGNATURES))
-    assert L.drt_abi_version() == 1
+    assert L.drt_abi_version() == 2
 
 
 def test_create_without_gpu_fails_loudly():
@@ -130,6 +130,30 @@ def test_camera_frame_matches_reference_golden():
         f = s.camera_frame()
         mine = np.array([f.plane_dist, f.aperture, f.w, f.h, *f.u, *f.v, *f.n], np.float32)
         np.testing.assert_array_equal(bits(mine), bits(g["cam_frames"][ci]))
+
+
+def test_set_eye_matches_oracle_camera(oracle_mod):
+    """Camera::SetEye (camera.h:63-72), the interactive camera motion (main.cpp:530-533): the host
+    camera and the oracle recompute the frame (u, v, n) and the plane distance bit for bit; the view
+    window (w, h) and the aperture keep their construction values, as in the reference."""
+    g = np.load(GOLD / "ref_misc.npz")
+    for ci, c in enumerate(g["cam_params"]):
+        a, b = drt.Scene(), oracle_mod.Scene.new()
+        for s in (a, b):
+            s.set_camera(c[0:3], c[3:6], c[6:9], c[9], c[10], int(c[11]), int(c[12]), c[13], c[14])
+        f0 = a.camera_frame()
+        for k in range(5):  # an orbit about the z axis through `at`, plus a change of height
+            ang = 0.7 * (k + 1)
+            e = np.array(c[0:3], np.float64) - np.array(c[3:6], np.float64)
+            eye = np.array(c[3:6], np.float64) + np.array([e[0] * np.cos(ang) - e[1] * np.sin(ang),
+                                                           e[0] * np.sin(ang) + e[1] * np.cos(ang), e[2] + 0.1 * k])
+            a.set_eye(eye)
+            b.set_eye(eye)
+            f = a.camera_frame()
+            mine = np.array([f.plane_dist, f.aperture, f.w, f.h, *f.u, *f.v, *f.n], np.float32)
+            np.testing.assert_array_equal(bits(mine), bits(b.camera_frame()), err_msg=f"camera {ci} eye {k}")
+            np.testing.assert_array_equal(np.float32(f.eye), np.float32(eye))
+            assert (f.w, f.h, f.aperture) == (f0.w, f0.h, f0.aperture)
 
 
 @needs_reference
