@@ -146,20 +146,16 @@ def interval_union(starts, ends):
     return tot
 
 
-def load_ceiling(working_set=None):
-    """The measured gather ceiling (profiles/gather_ceiling.json): the fastest table's rate (the
-    bound), and the rate for the smallest measured table that holds the scene's records (one chain
-    per lane, as the path kernel runs) as a same-size reference."""
+def load_ceiling():
+    """The measured ceilings of the path kernel's access shape (profiles/gather_ceiling.json,
+    tools/gather_ceiling.hip): dependent 64-B per-lane record gathers from an L1/L2-resident table
+    (the vector-memory path's own rate, the bound) and the L2 <-> fabric line rate of the same
+    gathers from a table past the caches (every record a 128-B line read)."""
     try:
         c = json.loads(CEILING_JSON.read_text())
-        out = {"peak_GB_per_s": c["peak_GB_per_s"], "table_bytes": c["peak_table_bytes"],
-               "source": "profiles/gather_ceiling.json (tools/gather_ceiling.hip)"}
-        rows = sorted((r for r in c.get("rows", []) if r.get("chains") == 1), key=lambda r: r["table_bytes"])
-        if working_set and rows:
-            fit = next((r for r in rows if r["table_bytes"] >= working_set), rows[-1])
-            out["same_size"] = {"table_bytes": fit["table_bytes"], "GB_per_s": fit["GB_per_s"],
-                                "scene_record_bytes": int(working_set)}
-        return out
+        return {"peak_GB_per_s": c["peak_GB_per_s"], "table_bytes": c["peak_table_bytes"],
+                "fabric_line_GB_per_s": c.get("fabric_line_GB_per_s"),
+                "source": "profiles/gather_ceiling.json (tools/gather_ceiling.hip)"}
     except Exception:
         return None
 
@@ -359,10 +355,7 @@ def main():
     bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
         PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-    # the scene's records: inner BVH nodes (64 B; a binary tree has (nodes - 1) / 2 of them) and
-    # primitives (48 B)
-    ceiling = load_ceiling(64 * max(0, (info.bvh_nodes - 1) // 2) + 48 * info.n_objects
-                           if args.accel == "bvh" else None)
+    ceiling = load_ceiling()
     traffic = None
     valu_busy = None
     dflt = {"aperture": 0.0, "focal": 1.0, "roughness": 0.0, "max_depth": 4, "light_spp": 1, "accel": "bvh", "ks": 0.5}
@@ -370,20 +363,37 @@ def main():
     head = f"tris{args.tris}" if args.scene == "synthetic" else args.scene
     workload_key = "_".join([f"{head}_res{args.res}_spp{args.spp}"] + extras)
     tj = Path(args.traffic_json)
+    pmc = {}
+    read_bytes = None
     if world == 1 and tj.exists():
         try:
-            tr = json.loads(tj.read_text())
-            if tr.get("workload") == workload_key:
+            # tools/pmc_traffic.py records one entry per workload key: fabric bytes per launch and the
+            # pipe ratios (VALU busy against the gfx950 issue peak: a wave64 VALU instruction occupies
+            # a SIMD for 2 cycles; kernel cycles = GRBM_GUI_ACTIVE / 8, the counter sums the 8 XCDs)
+            tr = json.loads(tj.read_text()).get("workloads", {}).get(workload_key)
+            if tr:
                 traffic = tr.get("hbm_bytes_per_launch")
-                # VALU busy against the gfx950 issue peak: a wave64 VALU instruction occupies a
-                # SIMD for 2 cycles (32 lanes/cycle: 157 TFLOP/s f32 = 1024 SIMDs x 2.4 GHz x 32 x
-                # 2); kernel cycles = GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs)
-                raw = tr.get("raw", {})
-                if raw.get("SQ_INSTS_VALU") and raw.get("GRBM_GUI_ACTIVE"):
-                    valu_busy = 2.0 * raw["SQ_INSTS_VALU"] / (1024.0 * raw["GRBM_GUI_ACTIVE"] / 8.0)
+                valu_busy = tr.get("valu_busy")
+                pmc = {k: round(tr[k], 4) for k in ("l1_hit_rate", "tcc_hit_rate", "ta_busy", "td_busy", "salu_per_valu")
+                       if tr.get(k) is not None}
+                pmc["read_bytes_method"] = tr.get("read_bytes_method")
+                read_bytes = tr.get("read_bytes")
         except Exception:
             traffic = None
 
+    # Two-level gather model of the path kernel: every record read costs the
+    # vector-memory path's L1/L2-resident gather rate, except the records that miss the L2, which
+    # cost the rate measured for gathers from a table past the caches.  Missed records = fabric line
+    # reads (128 B each, PMC) — one per missed 64-B record, as the calibration table measured.
+    model = None
+    if read_bytes and ceiling and ceiling.get("fabric_line_GB_per_s"):
+        miss = read_bytes / 128.0
+        hit_bytes = max(0.0, bytes_launch - 64.0 * miss)
+        t_hit = hit_bytes / (ceiling["peak_GB_per_s"] * 1e9) * 1e3
+        t_miss = 64.0 * miss / (ceiling["fabric_line_GB_per_s"] / 2.0 * 1e9) * 1e3
+        model = {"t_ms": round(t_hit + t_miss, 3), "t_l2_resident_ms": round(t_hit, 3),
+                 "t_fabric_ms": round(t_miss, 3), "missed_records": int(miss),
+                 "frac": round((t_hit + t_miss) / kernel_ms, 4)}
     value = rays_frame * args.steps / dt / 1e6
     out = {
         "metric": "Mrays/s + frame ms at 512x512x64spp, 1M-tri BVH scene, 1/2/4/8 MI355X",
@@ -409,18 +419,22 @@ def main():
                    "scene": args.scene, "tris": args.tris if args.scene == "synthetic" else 0, "res": args.res, "spp": args.spp, "accel": args.accel, "key": workload_key,
                    "parallelism": f"tile-shard x{world}" + (" + RCCL all-gather" if world > 1 else ""),
                    "frames_in_flight": pipe, "settle_frames": settle},
-        # bound: the per-CU vector-memory path serving dependent 64-B per-lane record gathers (TA/TD
-        # busy 98 %), peak = tools/gather_ceiling.hip's fastest table; achieved =
+        # bound: the per-CU vector-memory path serving dependent 64-B per-lane record gathers (TD
+        # busy 98 %), peak = tools/gather_ceiling.hip's L1/L2-resident rate; achieved =
         # algorithmic record bytes (64 B per inner-node visit + 48 B per primitive test) per second
-        # of path-kernel device time.  hbm_frac: PMC-measured fabric bytes per launch against 8 TB/s.
+        # of path-kernel device time.  traffic: PMC-measured L2 <-> fabric bytes per launch (reads
+        # from the request-size counters, tools/pmc_traffic.py); fabric_frac against the measured
+        # fabric line rate of the same gathers, hbm_frac against the 8 TB/s HBM figure.
         "roofline": {"bound": "vmem_gather", "achieved": round(achieved, 1),
                      "peak": ceiling["peak_GB_per_s"] if ceiling else None, "unit": "GB/s",
                      "frac": round(achieved / ceiling["peak_GB_per_s"], 4) if ceiling else None,
-                     "frac_same_size": round(achieved / ceiling["same_size"]["GB_per_s"], 4)
-                     if ceiling and "same_size" in ceiling else None,
                      "traffic": traffic,
+                     "fabric_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / ceiling["fabric_line_GB_per_s"], 4)
+                     if traffic and ceiling and ceiling.get("fabric_line_GB_per_s") else None,
                      "hbm_frac": round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                      "valu_busy": round(valu_busy, 4) if valu_busy else None,
+                     "pmc": pmc or None,
+                     "two_level_model": model,
                      "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),
                      "ceiling": ceiling},

@@ -731,6 +731,7 @@ __global__ void __launch_bounds__(kBlock) path_kernel(SceneArgs S, FrameArgs F) 
 // per-pixel reduce is unchanged, so frames are bit-identical.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;
+constexpr uint32_t kPartYield = 0xFFFFFFFFu;  // MODE_SEQ tail: the wave hands its pixels over
 
 // LDS traversal-stack entries per thread for a given occupancy target (5 blocks of 256 threads
 // fit 16 entries in 160 KiB; 6-8 blocks need a shorter LDS stack, the rest spills to scratch).
@@ -911,9 +912,11 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   if (STATS && !resume) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
   const size_t cidx = (size_t)ix + (size_t)nx * iy + (size_t)nx * ny * iz;
   uint32_t b = 0, e = 0;  // LF_EMPTY: the cell lies in an empty macro-cell (the last call's walk)
-  if (!(fl & LF_EMPTY)) {
-    b = resume ? L.spa : S.cell_start[cidx];
-    e = S.cell_start[cidx + 1];
+  if (!(fl & LF_EMPTY)) {  // the cell's range [start, next start) in one 8-B load (4-B aligned)
+    uint2 r;
+    __builtin_memcpy(&r, S.cell_start + cidx, sizeof(r));
+    b = resume ? L.spa : r.x;
+    e = r.y;
   }
   // the cell's objects in insertion order, two inline records (drt_upload_grid) per round trip
   bool done = false;
@@ -1086,6 +1089,12 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     s4 = rec[4];
     s5 = rec[5];
   }
+  // (Measured alternative, kept out (round 3): the quad-cooperative fetch — the 4 lanes of a quad
+  // load each other's records one 64-B segment per load instruction and transpose them with DPP
+  // quad_perm; tools/gather_ceiling.hip variant `quad_coop`.  1.37x the per-lane gather rate from
+  // an L1-resident table in isolation, but the path kernel ran 1 068 against 1 736 Mrays/s and the
+  // streaming traversal kernel 0.65-0.78x: the transpose's ~50 VALU and DPP hazards sit on each
+  // step's load -> test -> next-address chain, and the step must run with the whole wave active.)
   if (inner) {
     if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
     const float4 a = s0, b = s1, c = s2;
@@ -1601,6 +1610,11 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
   // [x * part_items, (x + 1) * part_items) — a band of tiles, so that XCD's L2 serves rays of
   // one screen region — and moves on to the next partition once that one is claimed.  Shards
   // the claim atomics over 8 words (MI355X_MICROARCH.md, dequeue); measured +0.3 %.
+  // (Measured alternative, kept out (round 3): one partition per CU — 32 per XCD, a CU's waves
+  // starting on a run of 4 consecutive tiles so that its L1 serves one small screen region, the CU's
+  // slot from a per-frame (XCC id, HW_ID) table, and a 64-lane scan of the next partitions' counters
+  // once a partition is used up: headline 1 677-1 711 against 1 692-1 743 Mrays/s, C3 / C4 / Grid
+  // within 0.3 %, and 17 more VGPR spills in the mixed-primitive AA kernel.)
   uint32_t part = __builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u, parts_done = 0;  // HW_REG_XCC_ID
   uint64_t cyc[4] = {0, 0, 0, 0};  // stats builds: refill / node / shading / leaf-block cycles (wave-uniform)
   // MODE_SEQ tail (F.seq_cont): a lane runs a whole pixel's samples in order, so once every pixel
@@ -1609,7 +1623,8 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
   // 4x the pixels per lane).  Waves numbered past what the unfinished pixels need hand their
   // pixels over at sample boundaries and exit; the waves kept take them from the slots.
   // No register is added to the loop for this (its allocation sits on an edge): a
-  // wave handing over sets `part` to 8 (no partition is claimed once the wave is exhausted), and
+  // wave handing over sets `part` to kPartYield (no partition is claimed once the wave is
+  // exhausted), and
   // the unfinished-pixel count is read from memory when it is needed.
   auto stamp = [&]() -> uint64_t {
     if (!STATS) return 0;
@@ -1638,12 +1653,12 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         if (base + rank < pn) lane_init<STATS, MODE, ACC>(S, F, L, pbeg + base + rank, C);
       }
     }
-    if (MODE == MODE_SEQ && exhausted && F.seq_cont && part != 8u) {
+    if (MODE == MODE_SEQ && exhausted && F.seq_cont && part != kPartYield) {
       const uint64_t idle2 = __ballot(L.item == kNoItem);
       const int n2 = __popcll(idle2);
       // About one iteration in sixteen (bits of the cycle counter), and on every try of a wave
       // with nothing to do: is this wave past the number the unfinished pixels need?  Then it
-      // hands its pixels over (part = 8) and exits once they are gone; with no pixel left, every
+      // hands its pixels over (part = kPartYield) and exits once they are gone; with no pixel left, every
       // wave is.  A wave with nothing to do otherwise waits here for a handed-over pixel, so that
       // the loop's exit test stays the one-line test of the other modes (a test there reading
       // the pixel count raised the loop's VGPR spills 103 -> 216 and made C4 frames 6x slower).
@@ -1660,7 +1675,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
           const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)(pblock<ACC>() / 64) +
                                                               (threadIdx.x >> 6));
           if ((uint64_t)wid * 6400u >= (uint64_t)left * (uint64_t)F.seq_slack) {
-            part = 8u;
+            part = kPartYield;
             break;
           }
         }
@@ -1733,7 +1748,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         if (done) C.v[ST_LANE_PATH_ITERS]++;
       }
       if (done) {
-        if (MODE == MODE_SEQ && part == 8u) L.fl |= LF_YIELD;
+        if (MODE == MODE_SEQ && part == kPartYield) L.fl |= LF_YIELD;
         lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
       }
     }

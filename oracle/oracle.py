@@ -343,12 +343,21 @@ class Scene:
 
 
 def host_threads():
-    """Every host core this process may run on (sched_getaffinity): the CPU baselines and the
-    full-size parity checks run the oracle on all of them, whatever OMP_NUM_THREADS says."""
+    """Every host core this process may use: the CPUs of its affinity set, capped by the cgroup
+    CPU quota (cpu.max) when one is set.  The CPU baselines and the full-size parity checks run the
+    oracle on all of them, whatever OMP_NUM_THREADS says.  (On the GPU boxes nproc is 256 under a
+    16-CPU quota; 256 OpenMP threads measured 5.1 Mrays/s there against 6.6-7.0 on 16.)"""
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return max(1, os.cpu_count() or 1)
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def keyed_rand(seed, pixel, k):

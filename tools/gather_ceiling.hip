@@ -57,8 +57,13 @@ __global__ void __launch_bounds__(kBlock, kWaves) gather(const float4* __restric
       const float4* r = table + 4 * (size_t)idx[c];
       const float4 a = r[0], b = r[1], d = r[2], e = r[3];
       acc += sum16(a, b, d, e);  // every dword is consumed, as a node test consumes its record
-      // the next record depends on this one (a BVH child descriptor does the same)
-      idx[c] = mix(idx[c] ^ __float_as_uint(a.x) ^ __float_as_uint(e.x)) & mask;
+      // the next record depends on this one (a BVH child descriptor does the same): slot 3's w is
+      // 0 in every record (set on the host, unknown to the compiler), so the address is a fresh
+      // uniform draw per (lane, step) that still waits for this load.  (Round 1-2's walk fed the
+      // record's data back into the hash: a random function of the index, whose chains merge onto
+      // cycles of ~sqrt(records) — after a few thousand steps the 128 MiB and 1 GiB tables were
+      // read from a few thousand L2-resident records.)
+      idx[c] = (mix((tid * 0x9E3779B9u) ^ mix(it * 2u + (uint32_t)c + 1u)) ^ __float_as_uint(e.w)) & mask;
     }
   }
   out[tid] = acc;
@@ -120,7 +125,7 @@ __global__ void __launch_bounds__(kBlock, kWaves) gather_coop(const float4* __re
     quad_transpose(X, Y);
     const float4 a = Y[0], b = Y[1], d = Y[2], e = Y[3];
     acc += sum16(a, b, d, e);
-    idx = mix(idx ^ __float_as_uint(a.x) ^ __float_as_uint(e.x)) & mask;
+    idx = (mix((tid * 0x9E3779B9u) ^ mix(it * 2u + 1u)) ^ __float_as_uint(e.w)) & mask;
   }
   out[tid] = acc;
 }
@@ -171,9 +176,9 @@ int main(int argc, char** argv) {
   const uint32_t max_rec = 1u << 24;
   std::vector<float> h(4 * 4 * (size_t)max_rec);
   uint32_t s = 12345u;
-  for (auto& v : h) {
+  for (size_t i = 0; i < h.size(); i++) {
     s = s * 1664525u + 1013904223u;
-    v = (float)(s >> 8) * (1.0f / 16777216.0f);
+    h[i] = (i % 16 == 15) ? 0.0f : (float)(s >> 8) * (1.0f / 16777216.0f);  // slot 3 .w = 0 (the walk)
   }
   float4* d_table = nullptr;
   float* d_out = nullptr;
