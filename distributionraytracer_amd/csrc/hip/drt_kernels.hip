@@ -919,6 +919,11 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
     e = r.y;
   }
   // the cell's objects in insertion order, two inline records (drt_upload_grid) per round trip
+  // (Measured alternative, kept out (round 3): 16-B per-cell records (start, end, first two object
+  // indices) over the scene-order primitives, so that an object's one record serves every cell it
+  // overlaps instead of 3.3 inline copies; later indices read two at a time beside the pair before.
+  // Same dependent round trips and bit-identical frames, but one more load per pair and 32 more VGPR
+  // spills: 916 against 1 298 Mrays/s on the 1M-triangle grid.)
   bool done = false;
   // triangle scenes: the test and the hit update as selects, no exec-mask branches per object
   // (+1.3 % Mrays/s on the Grid; the same test in the BVH leaf block measured -1.7 %)
@@ -1595,6 +1600,11 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
   FrameStack fs;
   Counters C;
   for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
+  // (Measured alternative, kept out (round 3): the material and light tables copied into LDS after
+  // the traversal stack, so shading reads them with ds_read instead of gathers queued behind the
+  // node step's on the TA/TD path.  The kernel-local SceneArgs copy this needs moved kernel
+  // arguments from SGPRs into VGPRs and left some table reads as flat loads: the headline kernel's
+  // VGPR spills went 67 -> 113.)
   if (ACC == ACC_GRID) {  // the macro-cell occupancy bitmap, once per block
     for (int w = threadIdx.x; w < S.gmacro_words; w += pblock<ACC>()) ((LdsU32*)lds_bytes)[w] = S.gmacro[w];
     __syncthreads();
