@@ -97,6 +97,8 @@ struct drt_ctx {
   DevBuf d_samples_s[DRT_FRAME_SLOTS], d_stats_s[DRT_FRAME_SLOTS], d_counter_s[DRT_FRAME_SLOTS], d_perm_s[DRT_FRAME_SLOTS];
   // MODE_SEQ tail continuation slots per frame slot (FrameArgs::seq_cont), one per resident lane
   DevBuf d_cont_s[DRT_FRAME_SLOTS];
+  // two-pass in-order frames: per sample slot its stream position, per slot and bounce its closest hit
+  DevBuf d_skel_rk_s[DRT_FRAME_SLOTS], d_skel_hits_s[DRT_FRAME_SLOTS];
   int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
@@ -521,6 +523,7 @@ struct Plan {
   ReduceArgs R;
   int tiles_y, n_tiles;
   bool persistent;      // path_persistent (BVH) instead of path_kernel
+  bool two_pass;        // in-order frame as MODE_SKEL + MODE_REPLAY (no refraction in the scene)
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -589,6 +592,20 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
     F.nsub = slots;
   }
   P.n_slots = (uint64_t)F.n_my_tiles * F.tile * F.tile * slots;
+  // In-order keyed-stream frames in two passes (FrameMode MODE_SKEL / MODE_REPLAY): a random draw's
+  // position in a pixel's stream depends only on the closest-hit chain of the samples before it,
+  // because shadow rays draw nothing.  Pass 1 runs the pixels' samples in order but traces only
+  // those chains; pass 2 runs every sample independently from its recorded position.  Without
+  // refraction a sample's chain is linear (one closest hit per bounce), so the record is max_depth
+  // + 1 hits per sample; a scene with a refracting material (trans == 1, main.cpp:471) keeps the
+  // one-pass MODE_SEQ frame, and so do frames whose record would pass kTwoPassMaxBytes.
+  P.two_pass = false;
+  if (P.persistent && F.mode == MODE_SEQ && env_int("DRT_SEQ_TWO_PASS", 1) != 0 &&
+      P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
+    bool refr = false;
+    for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
+    P.two_pass = !refr;
+  }
   ReduceArgs& R = P.R;
   R.nsub = slots;
   R.scale = scale;
@@ -698,7 +715,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     P.F.grid_pairs = std::max(1, env_int("DRT_GRID_PAIRS", 3));  // >= 1: a lane must make progress
     P.F.grid_walk = std::max(0, env_int("DRT_GRID_WALK", 5));
     // MODE_SEQ tail hand-over (`handover` above)
-    if (P.F.mode == MODE_SEQ && handover) {
+    if (P.F.mode == MODE_SEQ && handover && !P.two_pass) {
       c->slot_handover[slot] = true;
       if (!c->cus) DRT_HIP(c, hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
       const uint32_t cap = (uint32_t)std::max(1, c->cus) * 2048u;  // 32 waves of 64 lanes per CU at most
@@ -716,7 +733,25 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       P.F.seq_backlog = (uint32_t)std::max(0, env_int("DRT_SEQ_BACKLOG", 0));
     }  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
-  if (P.F.n_items) {
+  if (P.F.n_items && P.two_pass) {
+    DevBuf& d_rk = c->d_skel_rk_s[slot];
+    DevBuf& d_hits = c->d_skel_hits_s[slot];
+    DRT_HIP(c, d_rk.ensure(sizeof(uint32_t) * P.n_slots));
+    DRT_HIP(c, d_hits.ensure(sizeof(uint2) * P.n_slots * (uint64_t)(P.F.max_depth + 1)));
+    FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order
+    F1.mode = MODE_SKEL;
+    F1.skel_rk = d_rk.as<uint32_t>();
+    F1.skel_hits = d_hits.as<uint2>();
+    F1.seq_cont = nullptr;
+    launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
+    DRT_HIP(c, hipGetLastError());
+    FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
+    F2.mode = MODE_REPLAY;
+    F2.n_items = P.n_slots;
+    F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
+    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));
+    launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
+  } else if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
     else launch_path(S, P.F, c->accel, c->tri_only, stats, st);
   }
@@ -762,6 +797,7 @@ int drt_plan_frame(const drt_ctx* c, const drt_frame_params* p, drt_frame_plan* 
   out->mode = P.F.mode;
   out->persistent = P.persistent ? 1 : 0;
   out->tiles_in_shard = P.F.n_my_tiles;
+  out->passes = P.two_pass ? 2 : 1;
   return DRT_OK;
 }
 

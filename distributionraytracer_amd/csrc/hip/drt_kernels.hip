@@ -1231,7 +1231,7 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
 template <int MODE>
 __device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 V) {
   V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
-  if (MODE == MODE_SEQ || MODE == MODE_PROG) {
+  if (MODE == MODE_SEQ || MODE == MODE_PROG || MODE == MODE_SKEL || MODE == MODE_REPLAY) {
     KRng rng{F.seed, L.pmix, L.rk};
     R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
     L.rk = rng.k;
@@ -1240,8 +1240,24 @@ __device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 
   return normalize(R);
 }
 
-template <bool STATS, int ACC>
+template <bool STATS, int MODE, int ACC>
 __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C);
+
+// A closest-hit query of the path: traversed, or in MODE_REPLAY read back from pass 1's record of
+// this sample and bounce (the lane is ready at once; pass 1 counted the traversal).
+template <bool STATS, int MODE, int ACC>
+__device__ __forceinline__ void closest_query(const SceneArgs& S, const FrameArgs& F, Lane& L, const RayP& q,
+                                              Counters& C) {
+  if (MODE == MODE_REPLAY) {
+    const uint2 h = F.skel_hits[(size_t)L.item * (uint32_t)(F.max_depth + 1) + (uint32_t)(L.depth - 1)];
+    L.q = q;
+    L.best_t = __uint_as_float(h.x);
+    L.best_prim = h.y;
+    L.fl = (L.fl & LF_OUTSIDE) | (h.y != 0xFFFFFFFFu ? LF_HIT : 0u);
+    return;
+  }
+  start_query<STATS, ACC>(S, L, q, false, 0.0f, C);
+}
 
 // The persistent kernel's rayTracing() call frames, split by what the unwind reads back
 // (main.cpp:489-520).  Every parent needs the head: its accumulated colour, kr, material and
@@ -1293,7 +1309,7 @@ __device__ __forceinline__ void finish_sample(const SceneArgs& S, const FrameArg
         L.item = kNoItem;
         return;
       }
-      seq_start_sample<STATS, ACC>(S, F, L, C);
+      seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
       return;
     }
     if (F.seq_cont) atomicAdd(F.work_counter + kSeqDone, 1u);
@@ -1358,7 +1374,9 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       const float sin_i = length(Vt);
       const V3 tv = dvf(Vt, length(Vt));
       const float sin_t = eta * sin_i;
-      const bool has_refr = (m.trans == 1.0f && sin_t < 1.0f);
+      // MODE_REPLAY frames have no refracting material (the two-pass plan's condition): no refraction
+      // child, Fresnel or Beer code and no frame tails in that instantiation
+      const bool has_refr = MODE != MODE_REPLAY && (m.trans == 1.0f && sin_t < 1.0f);
       const bool has_refl = m.ks > 0.0f;
       V3 beer = mk(1.f, 1.f, 1.f);
       RayP child = L.q;
@@ -1399,7 +1417,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         L.ior1 = child_ior;
         L.ls = L.lightPos;
         L.depth++;
-        start_query<STATS, ACC>(S, L, child, false, 0.0f, C);
+        closest_query<STATS, MODE, ACC>(S, F, L, child, C);
         return;
       }
       c = cclamp(L.acc);
@@ -1413,7 +1431,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
   if (ACC == ACC_GRID) {
     while (L.fsp > 0) {
       FrameHead& f = fs.h[L.fsp - 1];
-      if ((f.flags & 1u) == 0u) {
+      if (MODE != MODE_REPLAY && (f.flags & 1u) == 0u) {
         const FrameTail& ft = fs.t[L.fsp - 1];
         V3 rc = cclamp(c);
         if ((f.flags & 2u) == 0u) rc = cmulc(rc, ft.beer);
@@ -1426,7 +1444,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
           L.ior1 = ft.ior1;
           L.ls = ft.lightPos;
           L.depth = L.fsp + 1;
-          start_query<STATS, ACC>(S, L, make_ray(add(ft.hitP, mul(ft.N, offset)), R), false, 0.0f, C);
+          closest_query<STATS, MODE, ACC>(S, F, L, make_ray(add(ft.hitP, mul(ft.N, offset)), R), C);
           return;
         }
         c = cclamp(f.acc);
@@ -1444,7 +1462,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
     const uint32_t flags = f.flags;
     V3 acc = f.acc;
     const float kr = f.kr;
-    if ((flags & 1u) == 0u) {  // refraction child returned (main.cpp:489-496)
+    if (MODE != MODE_REPLAY && (flags & 1u) == 0u) {  // refraction child returned (main.cpp:489-496)
       const FrameTail& ft = fs.t[L.fsp - 1];
       V3 rc = cclamp(c);
       if ((flags & 2u) == 0u) rc = cmulc(rc, ft.beer);
@@ -1456,7 +1474,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
         L.ior1 = ft.ior1;
         L.ls = ft.lightPos;
         L.depth = L.fsp + 1;
-        start_query<STATS, ACC>(S, L, make_ray(add(ft.hitP, mul(ft.N, offset)), R), false, 0.0f, C);
+        closest_query<STATS, MODE, ACC>(S, F, L, make_ray(add(ft.hitP, mul(ft.N, offset)), R), C);
         return;
       }
     } else if (flags & 8u) {  // reflection child returned, reflectDir.N > 0 (main.cpp:513-518)
@@ -1468,21 +1486,55 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
   finish_sample<STATS, MODE, ACC>(S, F, L, C, c);
 }
 
+// MODE_SKEL: the closest query of bounce L.depth of sample L.smp returned: record it.  A hit that
+// rayTracing() reflects from (depth <= MAX_DEPTH and Ks > 0, main.cpp:453-512; a two-pass scene has
+// no refraction) starts the mirror child with the sample's reflectDir draw, computed exactly as
+// lane_process does; otherwise the sample's closest-hit chain is complete and the pixel's next
+// sample starts from the stream position it reached.  Shadow rays and colours are pass 2's.
+template <bool STATS, int ACC>
+__device__ void skel_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
+  const bool hit = (L.fl & LF_HIT) != 0u;
+  const size_t slot = (size_t)L.item * F.nsub + L.smp;
+  F.skel_hits[slot * (uint32_t)(F.max_depth + 1) + (uint32_t)(L.depth - 1)] =
+      make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
+  if (hit && L.depth <= F.max_depth) {
+    const uint32_t mat = prim_material(S.prims[3 * L.best_prim]);
+    if (S.mats[mat].ks > 0.0f) {
+      const V3 hitP = add(L.q.o, mul(L.q.d, L.best_t));  // main.cpp:361
+      V3 N = normalize(prim_normal(S.prims, L.best_prim, L.q, L.best_t));
+      if (!(dot(L.q.d, N) < 0.0f)) N = neg(N);
+      const V3 V = neg(normalize(L.q.d));
+      const V3 R = reflect_dir<MODE_SKEL>(F, L, N, V);
+      L.depth++;
+      start_query<STATS, ACC>(S, L, make_ray(add(hitP, mul(N, 1e-4f)), R), false, 0.0f, C);
+      return;
+    }
+  }
+  if (++L.smp < (uint32_t)F.nsub) {
+    seq_start_sample<STATS, MODE_SKEL, ACC>(S, F, L, C);
+    return;
+  }
+  L.item = kNoItem;
+}
+
 // MODE_SEQ: start sample L.smp of pixel L.item (path_kernel's in-order loop, main.cpp:651-665,
 // or the Whitted light-sample loop with glossy reflection, main.cpp:683-697).  The samples of
 // a pixel go to samples[pixel * nsub + smp]; the ordered reduce sums them as the loop did.
-template <bool STATS, int ACC>
+template <bool STATS, int MODE, int ACC>
 __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
-  const Item it = decode_item(F, S.res_x, S.res_y, L.item, 1);
+  // MODE_REPLAY lanes hold a sample slot (pixel * nsub + sample), the others a pixel
+  const uint32_t pixel = MODE == MODE_REPLAY ? L.item / (uint32_t)F.nsub : L.item;
+  const Item it = decode_item(F, S.res_x, S.res_y, pixel, 1);
   L.depth = 1;
   L.fsp = 0;
   L.ior1 = 1.0f;
   L.fl = 0u;
-  if (STATS) C.v[ST_SAMPLES]++;
+  if (STATS && MODE != MODE_REPLAY) C.v[ST_SAMPLES]++;  // pass 1 counts the two-pass frame's samples
+  if (MODE == MODE_SKEL) F.skel_rk[(size_t)L.item * F.nsub + L.smp] = L.rk;
   RayP r;
   if (F.spp > 0) {
     float rx, ry, sx, sy;
-    const int pos = F.perm ? (int)F.perm[(size_t)L.item * F.spp + L.smp] : shuffle_source(F, L.pmix, (int)L.smp);
+    const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + L.smp] : shuffle_source(F, L.pmix, (int)L.smp);
     sample_prologue_at(F, L.pmix, (int)L.smp, pos, rx, ry, sx, sy);
     const float px = (float)it.x + rx, py = (float)it.y + ry;
     if (F.dof) {
@@ -1500,13 +1552,13 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
                            ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
                       : mk(0.5f, 0.5f, 0.0f);
   }
-  start_query<STATS, ACC>(S, L, r, false, 0.0f, C);
+  closest_query<STATS, MODE, ACC>(S, F, L, r, C);
 }
 
 // MODE_SEQ: start pixel `item` at sample smp with its keyed stream at call rk — a pixel just
 // claimed (smp 0, rk past the prologue) or one another wave handed over (seq_donate).  One call
 // site in the persistent loop for both, so the sample start is inlined there once.
-template <bool STATS, int ACC>
+template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void seq_begin(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item, uint32_t smp,
                                           uint32_t rk, Counters& C) {
   const Item it = decode_item(F, S.res_x, S.res_y, item, 1);
@@ -1520,7 +1572,7 @@ __device__ __forceinline__ void seq_begin(const SceneArgs& S, const FrameArgs& F
   L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
   L.smp = smp;
   L.rk = rk;
-  seq_start_sample<STATS, ACC>(S, F, L, C);
+  seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
 }
 __device__ __forceinline__ uint32_t seq_first_rk(const FrameArgs& F) {
   return F.spp > 0 ? 5u * F.spp - 1u : 0u;  // after the prologue's 4 spp + spp - 1 calls
@@ -1530,8 +1582,21 @@ template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F, Lane& L, uint32_t item,
                                           Counters& C) {
   L.item = item;
-  if (MODE == MODE_SEQ) {  // work item = pixel
-    seq_begin<STATS, ACC>(S, F, L, item, 0u, seq_first_rk(F), C);
+  if (MODE == MODE_SEQ || MODE == MODE_SKEL) {  // work item = pixel
+    seq_begin<STATS, MODE, ACC>(S, F, L, item, 0u, seq_first_rk(F), C);
+    return;
+  }
+  if (MODE == MODE_REPLAY) {  // work item = sample slot: the sample from its recorded stream position
+    const Item it = decode_item(F, S.res_x, S.res_y, item, F.nsub);
+    if (!it.valid) {  // padding of a partial tile
+      F.samples[item] = make_float4(0.f, 0.f, 0.f, 0.f);
+      L.item = kNoItem;
+      return;
+    }
+    L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+    L.smp = (uint32_t)it.sub;
+    L.rk = F.skel_rk[item];
+    seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
     return;
   }
   if (MODE == MODE_PROG) {  // work item = pixel, one sample (main.cpp:540-572)
@@ -1751,7 +1816,9 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
     // in-order (MODE_SEQ) frames reach that point with each lane still holding a pixel's
     // remaining samples, so they keep batching until half the live lanes are ready (C4:
     // shading SIMD efficiency 0.10 -> 0.33, +2.7 %; on MODE_AA the same rule costs 1.4 %).
-    const bool drain = MODE == MODE_SEQ ? (exhausted && 2 * __popcll(ready) >= __popcll(ready | trav)) : exhausted;
+    const bool drain = (MODE == MODE_SEQ || MODE == MODE_SKEL)
+                           ? (exhausted && 2 * __popcll(ready) >= __popcll(ready | trav))
+                           : exhausted;
     if (ready && (__popcll(ready) >= F.process_min || trav == 0 || drain)) {
       if (STATS) {
         if (lane == 0) C.v[ST_WAVE_PATH_ITERS]++;
@@ -1759,7 +1826,8 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
       }
       if (done) {
         if (MODE == MODE_SEQ && part == kPartYield) L.fl |= LF_YIELD;
-        lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
+        if constexpr (MODE == MODE_SKEL) skel_process<STATS, ACC>(S, F, L, C);
+        else lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
       }
     }
     if (STATS) {
@@ -2061,6 +2129,8 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
     case MODE_AA: launch_persistent_m<T, ST, MODE_AA, A>(S, F, st); break;
     case MODE_WHITTED_QUAD: launch_persistent_m<T, ST, MODE_WHITTED_QUAD, A>(S, F, st); break;
     case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ, A>(S, F, st); break;
+    case MODE_SKEL: launch_persistent_m<T, ST, MODE_SKEL, A>(S, F, st); break;
+    case MODE_REPLAY: launch_persistent_m<T, ST, MODE_REPLAY, A>(S, F, st); break;
     case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG, A>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT, A>(S, F, st); break;
   }

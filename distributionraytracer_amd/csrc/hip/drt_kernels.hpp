@@ -14,7 +14,14 @@ enum FrameMode : int {
   MODE_SEQ = 1,           // one thread per pixel, samples in order with the keyed RNG stream
   MODE_WHITTED_QUAD = 2,  // one thread per (pixel, regular light sample): main.cpp:683-697
   MODE_WHITTED_POINT = 3,  // one thread per pixel: main.cpp:698-701
-  MODE_PROG = 4            // progressive zone A: one jittered sample per pixel, main.cpp:540-586
+  MODE_PROG = 4,           // progressive zone A: one jittered sample per pixel, main.cpp:540-586
+  // An in-order keyed-stream frame (MODE_SEQ) of a scene without refraction, in two passes:
+  MODE_SKEL = 5,    // pass 1, one lane per pixel, samples in order: only the closest-hit chain of
+                    // each sample (primary ray, mirror bounces) — which fixes every random draw's
+                    // position — recording each sample's stream position and each bounce's hit
+  MODE_REPLAY = 6   // pass 2, one lane per (pixel, sample), any order: the whole rayTracing() of
+                    // the sample from its recorded stream position, closest hits read back, shadow
+                    // rays traced
 };
 
 enum StatSlot : int {
@@ -49,6 +56,8 @@ constexpr size_t kMacroBits = 131072;  // Grid macro-cell bitmap budget: 16 KB o
 constexpr size_t kPrimPadBytes = 64;  // zeroed tail of the primitive buffer (node_step's slot reads)
 // persistent kernels: 32-bit work-item counters; bigger frames run the 64-bit path_kernel
 constexpr uint64_t kPersistentMaxItems = 0xF0000000ull;
+// two-pass in-order frames: the closest-hit record (8 B per sample and bounce) stays below this
+constexpr uint64_t kTwoPassMaxBytes = 32ull << 30;
 
 struct SceneArgs {
   // Camera (camera.h:32-61), precomputed on the host
@@ -118,6 +127,11 @@ struct FrameArgs {
   int seq_slack;               // waves kept = ceil(unfinished pixels * seq_slack / 100 / 64)
   int seq_pop_min;             // a kept wave takes handed-over pixels once this many lanes are idle
   uint32_t seq_backlog;        // a lane keeps its pixel while this many wait in the slots (0: no bound)
+  // MODE_SKEL / MODE_REPLAY: per sample slot (pixel * nsub + sample) its keyed-stream position at
+  // the sample's start, and per slot and depth (max_depth + 1 entries) the closest hit of that
+  // bounce: (t bits, primitive record), primitive 0xFFFFFFFF = miss
+  uint32_t* skel_rk;
+  uint2* skel_hits;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

@@ -611,6 +611,7 @@ def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, mo
     s.build()
     renderer.upload(s)
     kw = {"roughness": 0.1, "max_depth": 8}
+    monkeypatch.setenv("DRT_SEQ_TWO_PASS", "0")  # the one-pass in-order frame (the two-pass one has no tail)
     monkeypatch.setenv("DRT_SEQ_DONATE", "0")
     ref = renderer.render(seed=13, stats=True, **kw)
     rst = renderer.stats()
@@ -666,3 +667,43 @@ def test_slot_reused_from_another_stream_waits_for_its_last_frame(drt, renderer,
     torch.cuda.synchronize()
     for i in range(n):
         np.testing.assert_array_equal(outs[i].cpu().numpy().view(np.uint32), lone[i].view(np.uint32), err_msg=str(i))
+
+
+@pytest.mark.parametrize("accel,spp,kw", [("bvh", 16, {"roughness": 0.1, "max_depth": 8}), ("grid", 9, {"roughness": 0.2}),
+                                          ("bvh", 0, {"roughness": 0.2})])
+def test_two_pass_in_order_frame_equals_one_pass(drt, renderer, tmp_path, monkeypatch, accel, spp, kw):
+    """In-order keyed-stream frames (DoF / glossy) of scenes without refraction run in two passes
+    (drt_capi.hip plan, FrameMode MODE_SKEL / MODE_REPLAY): the pixels' closest-hit chains with the
+    samples in order, then every sample on its own from its recorded stream position with its
+    closest hits read back.  The frame and every ray / node / primitive count equal the one-pass
+    frame's (DRT_SEQ_TWO_PASS=0) bit for bit — AA with DoF, depth 8 and glossy bounces on the BVH,
+    the Grid, and the Whitted light-sample loop (spp 0) with glossy reflection — and a scene with a
+    refracting material keeps the one-pass frame."""
+    import bench
+
+    if spp:
+        s = drt.Scene()
+        bench.populate(s, bench.synthetic_triangles(50_000), 64, spp, aperture=8.0 if accel == "bvh" else 0.0,
+                       focal=1.0, accel=accel)
+        s.build()
+    else:  # the Whitted case on a mixed scene made refraction-free (every material's T set to 0)
+        import re
+        text = sg.mixed_scene_text(res=(32, 24), spp=0, accel=accel, n_tris=80)
+        text = "\n".join(re.sub(r"^(mat\s+(?:\S+\s+){9})\S+", r"\g<1>0", l) for l in text.split("\n"))
+        s = drt.Scene.load_p3f(sg.write(tmp_path, "s.p3f", text))
+    renderer.upload(s)
+    assert renderer.plan(renderer.frame_params(seed=5, **kw))["passes"] == 2
+    img = renderer.render(seed=5, stats=True, **kw)
+    st = renderer.stats()
+    monkeypatch.setenv("DRT_SEQ_TWO_PASS", "0")
+    assert renderer.plan(renderer.frame_params(seed=5, **kw))["passes"] == 1
+    ref = renderer.render(seed=5, stats=True, **kw)
+    rst = renderer.stats()
+    np.testing.assert_array_equal(bits(img), bits(ref))
+    for k in ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
+              "closest_prims", "shadow_prims", "samples"):
+        assert st[k] == rst[k], k
+    monkeypatch.delenv("DRT_SEQ_TWO_PASS")
+    glass = sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", n_tris=40, aperture=8.0, focal=1.5)
+    renderer.upload(drt.Scene.load_p3f(sg.write(tmp_path, "glass.p3f", glass)))
+    assert renderer.plan(renderer.frame_params(seed=5, roughness=0.1))["passes"] == 1
