@@ -747,6 +747,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DRT_HIP(c, hipGetLastError());
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
     F2.mode = MODE_REPLAY;
+    F2.waves = P.F.waves;
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));
