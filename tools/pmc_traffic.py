@@ -45,6 +45,23 @@ def timed_path_dispatch(counters, sub=None):
     return keys[-1] if keys else None
 
 
+def _targs(name):
+    try:
+        return [a.strip() for a in name.split("<", 2)[1].split(">")[0].split(",")]
+    except IndexError:
+        return []
+
+
+def _mode(name):
+    a = _targs(name)
+    return int(a[2]) if "path_persistent<" in name and len(a) > 2 and a[2].isdigit() else None
+
+
+def _stats(name):
+    a = _targs(name)
+    return len(a) > 1 and a[1] == "true"
+
+
 def derive(vals):
     """Fabric bytes and the pipe ratios bench.py reports, from the merged counters."""
     res = {}
@@ -97,7 +114,16 @@ def main():
         if k is None:
             continue
         kernel = k[1]
-        vals.update(c[k])
+        cur = dict(c[k])
+        # a two-pass in-order frame (FrameMode 5 then 6, drt_capi.hip): the frame is both launches
+        if _mode(k[1]) == 6:
+            prev = [d for d in c if d[0] < k[0] and _mode(d[1]) == 5 and not _stats(d[1])]
+            if prev:
+                p5 = max(prev)
+                kernel = p5[1] + " + " + k[1]
+                for n, v in c[p5].items():
+                    cur[n] = cur.get(n, 0.0) + v
+        vals.update(cur)
     rec = derive(vals)
     if "hbm_bytes_per_launch" not in rec:
         sys.exit(f"no read-byte counters under {root}: {sorted(vals)}")
