@@ -348,20 +348,89 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
     }
   }
   if (n_obj > kFirstMask) DRT_FAIL(c, DRT_E_UNSUPPORTED, "more than %u objects", kFirstMask);
+  // Where each inner record sits in memory (DRT_NODE_LAYOUT; the tree, its descriptors' meaning and
+  // every traversal are unchanged): 0 = reference node order; 1 (default) = a record and, in the
+  // same 128-B line, the record of its child with the larger box surface (the child a ray more
+  // often visits next), each such pair starting a line; 2 = a node's two inner children side by
+  // side, the pair starting a line.  Headline frame: fabric line reads 2.12 -> 1.89 G per launch
+  // with 1 (2: 2.11 G), 89.4 against 89.7 ms; C4 610-623 against 625 ms.
+  const int layout = env_int("DRT_NODE_LAYOUT", 1);
+  std::vector<uint32_t> slot_of(n_inner);
+  uint32_t n_slots = n_inner;
+  if ((layout == 1 || layout == 2) && n_inner > 0) {  // (a leaf root has no inner record)
+    auto area = [&](uint32_t i) {
+      const drt_bvh_node& nd = nodes[i];
+      const double x = (double)nd.bmax[0] - nd.bmin[0], y = (double)nd.bmax[1] - nd.bmin[1],
+                   z = (double)nd.bmax[2] - nd.bmin[2];
+      return x * y + y * z + z * x;
+    };
+    auto inner_children = [&](uint32_t n, uint32_t& a, uint32_t& b) {  // a: larger surface
+      const uint32_t l = nodes[n].index, r = l + 1;
+      a = b = UINT32_MAX;
+      const bool li = !nodes[l].leaf, ri = !nodes[r].leaf;
+      if (li && ri) {
+        a = area(l) >= area(r) ? l : r;
+        b = a == l ? r : l;
+      } else if (li) {
+        a = l;
+      } else if (ri) {
+        a = r;
+      }
+    };
+    uint32_t pos = 0;
+    std::vector<uint32_t> st;
+    if (layout == 1) {
+      st.push_back(0u);
+      while (!st.empty()) {
+        const uint32_t n = st.back();
+        st.pop_back();
+        pos += pos & 1u;  // a line starts
+        slot_of[rec[n]] = pos++;
+        uint32_t a, b;
+        inner_children(n, a, b);
+        if (a == UINT32_MAX) continue;
+        slot_of[rec[a]] = pos++;
+        if (b != UINT32_MAX) st.push_back(b);
+        uint32_t aa, ab;
+        inner_children(a, aa, ab);
+        if (ab != UINT32_MAX) st.push_back(ab);
+        if (aa != UINT32_MAX) st.push_back(aa);
+      }
+    } else {
+      slot_of[rec[0]] = pos++;
+      st.push_back(0u);
+      while (!st.empty()) {
+        const uint32_t n = st.back();
+        st.pop_back();
+        uint32_t a, b;
+        inner_children(n, a, b);
+        if (a == UINT32_MAX) continue;
+        pos += pos & 1u;
+        const uint32_t l = nodes[n].index;  // left, right order within the pair
+        if (!nodes[l].leaf) slot_of[rec[l]] = pos++;
+        if (!nodes[l + 1].leaf) slot_of[rec[l + 1]] = pos++;
+        if (b != UINT32_MAX) st.push_back(b);
+        st.push_back(a);
+      }
+    }
+    n_slots = pos;
+  } else {
+    for (uint32_t k = 0; k < n_inner; k++) slot_of[k] = k;
+  }
   std::vector<uint2> big;
   auto desc_of = [&](uint32_t i) -> uint32_t {
     const drt_bvh_node& nd = nodes[i];
-    if (!nd.leaf) return (uint32_t)rec[i];
+    if (!nd.leaf) return slot_of[(size_t)rec[i]];
     if (nd.n_objs < kBigLeaf) return leaf_desc(nd.index, nd.n_objs);
     big.push_back(make_uint2(nd.index, nd.n_objs));
     return leaf_desc((uint32_t)big.size() - 1, kBigLeaf);
   };
-  std::vector<NodeRecord> recs(n_inner);
+  std::vector<NodeRecord> recs(n_slots);  // padding slots stay zero (never referenced)
   for (uint32_t i = 0; i < n_nodes; i++) {
     if (nodes[i].leaf) continue;
     const drt_bvh_node& L = nodes[nodes[i].index];
     const drt_bvh_node& R = nodes[nodes[i].index + 1];
-    NodeRecord& r = recs[rec[i]];
+    NodeRecord& r = recs[slot_of[(size_t)rec[i]]];
     const float b[12] = {L.bmin[0], L.bmin[1], L.bmin[2], L.bmax[0], L.bmax[1], L.bmax[2],
                          R.bmin[0], R.bmin[1], R.bmin[2], R.bmax[0], R.bmax[1], R.bmax[2]};
     memcpy(r.box, b, sizeof(b));

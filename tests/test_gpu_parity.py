@@ -591,6 +591,31 @@ def test_grid_stepper_caps_do_not_change_the_frame(drt, renderer, monkeypatch, w
         assert st[k] == rst[k], k
 
 
+@pytest.mark.parametrize("layout", ["0", "2"])
+def test_node_record_layout_does_not_change_the_frame(drt, renderer, monkeypatch, layout):
+    """Where drt_upload_bvh puts each inner node record in memory (DRT_NODE_LAYOUT: 1, the default,
+    pairs a record with its larger child's in one 128-B line; 0 keeps the reference's node order;
+    2 pairs siblings) changes only addresses: on the 1M-triangle scene, AA and glossy in-order frames
+    and every ray, node, leaf and primitive count equal the default layout's bit for bit."""
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(1_000_000), 96, 4)
+    s.build()
+    keys = ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
+            "closest_prims", "shadow_prims", "samples")
+    out = {}
+    for lay in ("1", layout):
+        monkeypatch.setenv("DRT_NODE_LAYOUT", lay)
+        renderer.upload(s)
+        out[lay] = [(bits(renderer.render(seed=3, stats=True, **kw)), renderer.stats())
+                    for kw in ({}, {"roughness": 0.1, "max_depth": 6})]
+    for (img, st), (ref, rst) in zip(out[layout], out["1"]):
+        np.testing.assert_array_equal(img, ref)
+        for k in keys:
+            assert st[k] == rst[k], k
+
+
 @pytest.mark.parametrize("accel", ["bvh", "grid"])
 def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, monkeypatch, accel):
     """MODE_SEQ frames (DoF + glossy: a lane runs a pixel's samples in order) hand pixels between
