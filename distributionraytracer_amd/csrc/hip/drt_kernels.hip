@@ -900,7 +900,13 @@ __device__ __forceinline__ DdaState dda_step(DdaState d, const DdaAxes& a, bool 
 // when best.t < t_next of the stepped axis, leaving the grid is a miss (even with a farther hit).
 // (Measured alternative, kept out: one memory round trip per iteration — the cell range, or two
 // objects with the next cell's range prefetched speculatively — 6-17 % slower than a whole cell
-// per iteration.)
+// per iteration.  Round 3: the same stream inside one call — up to R rounds, each giving every
+// lane one unit of memory work in shared load instructions (its next two objects, or its new
+// cell's range through the first object slot), with the DDA step and a capped walk per round:
+// 1.1-1.2 G vector-memory instructions fewer and a third less waiting, but SALU 41 -> 57-67 G and
+// LDS 0.25 -> 0.69 G (the walk and its macro-cell lookups once per round): 1 010-1 090 against
+// 1 292 Mrays/s at every (R, walk) tried, branch-free loads included
+// (profiles/r03_grid_stream_ab.jsonl).  Cells and records in macro-cell-bricked order: neutral.)
 template <bool TRI_ONLY, bool STATS>
 __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters& C, const LdsU32* macro, int walk,
                                           int pairs) {
