@@ -906,7 +906,11 @@ __device__ __forceinline__ DdaState dda_step(DdaState d, const DdaAxes& a, bool 
 // 1.1-1.2 G vector-memory instructions fewer and a third less waiting, but SALU 41 -> 57-67 G and
 // LDS 0.25 -> 0.69 G (the walk and its macro-cell lookups once per round): 1 010-1 090 against
 // 1 292 Mrays/s at every (R, walk) tried, branch-free loads included
-// (profiles/r03_grid_stream_ab.jsonl).  Cells and records in macro-cell-bricked order: neutral.)
+// (profiles/r03_grid_stream_ab.jsonl).  Cells and records in macro-cell-bricked order: neutral.
+// A 64-bit occupancy mask per macro-cell, read beside a cell's range once per macro-cell and held
+// in two VGPRs, so that the walk also steps through the empty cells of non-empty macro-cells
+// (36-48 % of their cells) without loading their ranges: bit-identical, but VGPR spills 102 ->
+// 115 and 1 047 against 1 300 Mrays/s; 3-11 % slower on the shipped Grid scenes too.)
 template <bool TRI_ONLY, bool STATS>
 __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters& C, const LdsU32* macro, int walk,
                                           int pairs) {
