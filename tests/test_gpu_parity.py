@@ -49,6 +49,20 @@ def compare_images(img, ref, tol=TOL):
     return exact
 
 
+def assert_same_work(accel, st, rst):
+    """Identical branching => identical traversal work: rays on every accelerator; on the BVH
+    inner-node visits, leaf visits and primitive tests (bvh.cpp:245-312); on the Grid the cells
+    examined (leaf) and the objects tested in them (grid.cpp:262-273)."""
+    if accel == 0:
+        return
+    assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
+    keys = ("closest_leaf", "shadow_leaf", "closest_prims", "shadow_prims")
+    if accel == 2:
+        keys += ("closest_inner", "shadow_inner")
+    for k in keys:
+        assert st[k] == rst[k], (k, st[k], rst[k])
+
+
 GOLD_CASES = ["tiny", "mixed", "tris2k"]
 
 
@@ -163,13 +177,7 @@ def test_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
     ref, rst = b.render(seed=seed, **kw)
     compare_images(img, ref)
     # identical branching => identical traversal work
-    if a.info().accel != 0:
-        assert st["closest_rays"] == rst["closest_calls"]
-        assert st["shadow_rays"] == rst["shadow_calls"]
-    if a.info().accel == 2:
-        assert st["closest_inner"] == rst["closest_inner"] and st["closest_leaf"] == rst["closest_leaf"]
-        assert st["shadow_inner"] == rst["shadow_inner"] and st["shadow_leaf"] == rst["shadow_leaf"]
-        assert st["closest_prims"] == rst["closest_prims"] and st["shadow_prims"] == rst["shadow_prims"]
+    assert_same_work(a.info().accel, st, rst)
     assert st["samples"] == rst["samples"]
 
 
@@ -412,8 +420,11 @@ def test_full_size_config_matches_oracle(drt, oracle_mod, renderer, case):
     b.build()
     thr = oracle_mod.host_threads()
     if rows is None:
-        ref, _ = b.render(seed=7, threads=thr, **kw)
+        ref, rst = b.render(seed=7, threads=thr, **kw)
         compare_images(img, ref)
+        # and the whole frame's traversal work equals the oracle's (the stats build of the kernel)
+        renderer.render(seed=7, stats=True, **kw)
+        assert_same_work(a.info().accel, renderer.stats(), rst)
         return
     for y in rows:
         ref, _ = b.render(seed=7, rows=(y, y + 1), threads=thr, **kw)

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from tests import shipped
-from tests.test_gpu_parity import TOL, compare_images
+from tests.test_gpu_parity import TOL, assert_same_work, compare_images
 
 pytestmark = pytest.mark.gpu
 
@@ -68,12 +68,7 @@ def test_shipped_scene_matches_oracle(drt, oracle_mod, renderer, tmp_path, case)
     ref, rst = b.render(seed=2718, **kw)
     exact = compare_images(img, ref, TOL)
     assert exact > 0.5, f"only {exact:.3f} of the channels are bit-identical"
-    acc = a.info().accel
-    if acc != 0:
-        assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
-    if acc == 2:
-        for k in ("closest_inner", "closest_leaf", "shadow_inner", "shadow_leaf", "closest_prims", "shadow_prims"):
-            assert st[k] == rst[k], k
+    assert_same_work(a.info().accel, st, rst)
     assert st["samples"] == rst["samples"]
     if shipped.env(name):  # the sky, not bclr, fills the misses
         assert a.info().skybox_loaded
