@@ -63,6 +63,14 @@ def assert_same_work(accel, st, rst):
         assert st[k] == rst[k], (k, st[k], rst[k])
 
 
+def assert_same_work_frame(renderer, img, rst, seed, **kw):
+    """Re-render a frame with the kernel's stats build: the same frame bit for bit, and the
+    oracle's traversal work (assert_same_work)."""
+    img_s = renderer.render(seed=seed, stats=True, **kw)
+    np.testing.assert_array_equal(bits(img_s), bits(img))
+    assert_same_work(renderer.scene.info().accel, renderer.stats(), rst)
+
+
 GOLD_CASES = ["tiny", "mixed", "tris2k"]
 
 
@@ -196,8 +204,7 @@ def test_progressive_matches_oracle(drt, oracle_mod, renderer, tmp_path, accel, 
         _, rst = b.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_o)
         compare_images(acc_g, acc_o)
         assert st["samples"] == rst["samples"] == 24 * 16
-        if accel != "none":
-            assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
+        assert_same_work(a.info().accel, st, rst)
     before = acc_g.copy()
     renderer.render(seed=9, progressive_frame=10000, accum=acc_g)  # MAX_SAMPLES: untouched
     np.testing.assert_array_equal(acc_g, before)
@@ -296,8 +303,9 @@ def test_reference_scene_balls_low_bvh(drt, oracle_mod, renderer, tmp_path):
     a, b = load_both(drt, oracle_mod, tmp_path, text)
     renderer.upload(a)
     img = renderer.render(seed=99)
-    ref, _ = b.render(seed=99)
+    ref, rst = b.render(seed=99)
     compare_images(img, ref)
+    assert_same_work_frame(renderer, img, rst, 99)
 
 
 def test_full_size_frame_properties(drt, renderer, tmp_path):
@@ -423,8 +431,7 @@ def test_full_size_config_matches_oracle(drt, oracle_mod, renderer, case):
         ref, rst = b.render(seed=7, threads=thr, **kw)
         compare_images(img, ref)
         # and the whole frame's traversal work equals the oracle's (the stats build of the kernel)
-        renderer.render(seed=7, stats=True, **kw)
-        assert_same_work(a.info().accel, renderer.stats(), rst)
+        assert_same_work_frame(renderer, img, rst, 7, **kw)
         return
     for y in rows:
         ref, _ = b.render(seed=7, rows=(y, y + 1), threads=thr, **kw)
@@ -447,8 +454,9 @@ def test_skybox_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, accel
     b = oracle_mod.Scene.load_p3f(p, skybox_faces=faces)
     renderer.upload(a)
     img = renderer.render(seed=5)
-    ref, _ = b.render(seed=5)
+    ref, rst = b.render(seed=5)
     compare_images(img, ref)
+    assert_same_work_frame(renderer, img, rst, 5)
     bg = np.array([0.078, 0.361, 0.753], np.float32)
     assert (np.abs(img - bg).max(axis=-1) > 1e-3).mean() > 0.9  # the sky, not bclr, fills the misses
 
@@ -466,8 +474,9 @@ def test_edge_scene_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
     a, b = load_both(drt, oracle_mod, tmp_path, EDGE_CASES[case]())
     renderer.upload(a)
     img = renderer.render(seed=3)
-    ref, _ = b.render(seed=3)
+    ref, rst = b.render(seed=3)
     compare_images(img, ref)
+    assert_same_work_frame(renderer, img, rst, 3)
     np.testing.assert_allclose(img, np.broadcast_to(np.float32([0.078, 0.361, 0.753]), img.shape), atol=1e-6)
 
 
@@ -480,8 +489,9 @@ def test_no_lights_and_deepest_recursion_match_oracle(drt, oracle_mod, renderer,
     renderer.upload(a)
     for kw in ({}, {"max_depth": 15}):
         img = renderer.render(seed=8, **kw)
-        ref, _ = b.render(seed=8, **kw)
+        ref, rst = b.render(seed=8, **kw)
         compare_images(img, ref)
+        assert_same_work_frame(renderer, img, rst, 8, **kw)
 
 
 @pytest.mark.parametrize("pipe,aux", [(2, "0"), (2, "1"), (4, "1")])
