@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes of the timed path-kernel dispatch for every BASELINE config on one GPU (headline, C3,
-# C4, the headline scene on the Grid), one rocprofv3 run per counter group, merged per workload key
+# C4, the headline scene on the Grid, C2), one rocprofv3 run per counter group, merged per workload key
 # into profiles/pmc_traffic.json (tools/pmc_traffic.py; bench.py reads its key's record).
 set -u
 export TMPDIR=/tmp
@@ -12,9 +12,12 @@ GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum T
   "TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TD_TD_BUSY TD_TC_STALL GRBM_GUI_ACTIVE"
   "TCP_TOTAL_CACHE_ACCESSES TCP_PENDING_STALL_CYCLES TCP_TCC_READ_REQ TCP_TCC_READ_REQ_LATENCY")
 CONFIGS=("headline:" "c3:--tris 100000 --light-spp 4" "grid:--accel grid"
-  "c4:--res 1024 --aperture 8 --focal 1 --roughness 0.1 --max-depth 8")
+  "c4:--res 1024 --aperture 8 --focal 1 --roughness 0.1 --max-depth 8" "c2:--scene balls_low --spp 16")
 for cfg in "${CONFIGS[@]}"; do
-  name=${cfg%%:*}; args=${cfg#*:}; mkdir -p $OUT/$name
+  name=${cfg%%:*}; args=${cfg#*:}
+  # PMC_ONLY="c2 grid": only those configs (their records are merged into the existing database)
+  if [ -n "${PMC_ONLY:-}" ] && [[ " $PMC_ONLY " != *" $name "* ]]; then continue; fi
+  mkdir -p $OUT/$name
   i=0
   for grp in "${GROUPS_[@]}"; do
     i=$((i+1))
