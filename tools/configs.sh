@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT; : > $OUT/configs.jsonl
 run() {  # name, bench args...
   local name=$1; shift
-  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 8 "$@" > $OUT/cfg_$name.json 2> $OUT/cfg_$name.err
+  timeout -k 10 300 python bench.py --steps ${CFG_STEPS:-3} --warmup 1 --cpu-seconds 8 "$@" > $OUT/cfg_$name.json 2> $OUT/cfg_$name.err
   local rc=$?
   echo "{\"config\": \"$name\", \"rc\": $rc, \"line\": $(cat $OUT/cfg_$name.json 2>/dev/null || echo null)}" >> $OUT/configs.jsonl
   echo "$name rc=$rc $(cut -c1-160 $OUT/cfg_$name.json)"
