@@ -263,3 +263,19 @@ def test_group_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError, match="drt_group_create"):
         drt.RendererGroup([0])
+
+
+def test_grid_vs_bvh_tool_covers_the_shipped_grid_scenes(tmp_path):
+    """SURVEY §8 f4 motivates the Grid kernel's perf row by the shipped scenes whose P3F selects
+    `accel grid`; tools/grid_vs_bvh.py (profiles/r03_grid_vs_bvh_shipped.jsonl) must time exactly
+    those, and each must load with the Grid as its accelerator (scene.h:22, accel 1)."""
+    from tests import shipped
+
+    text = (ROOT / "tools" / "grid_vs_bvh.py").read_text()
+    scenes = set(re.findall(r'"(\w+)"', re.search(r"SCENES = \(([^)]*)\)", text).group(1)))
+    grid_default = {n for n in shipped.names()
+                    if re.search(rb"(?m)^accel[ \t]+grid", shipped._npz()[f"{n}/head"].tobytes())}
+    assert scenes == grid_default, (scenes, grid_default)
+    for n in sorted(grid_default):
+        s = drt.Scene.load_p3f(shipped.write(tmp_path, n), skybox_faces=shipped.skybox_faces(n))
+        assert s.info().accel == 1, n
