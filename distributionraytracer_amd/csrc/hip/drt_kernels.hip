@@ -752,7 +752,8 @@ enum LaneFlag : uint32_t {
   LF_EMPTY = 64u,   // Grid: the current cell lies in an empty macro-cell (no range load needed)
   LF_INCELL = 128u, // Grid: objects of the current cell left, from record L.spa on
   LF_YIELD = 256u,  // MODE_SEQ tail: the lane's wave is handing its pixels over (set per shading pass)
-  LF_RESUME = 512u  // MODE_SEQ tail: the lane took over a pixel; its next sample starts in finish_sample
+  LF_RESUME = 512u, // MODE_SEQ tail: the lane took over a pixel; its next sample starts in finish_sample
+  LF_LEAFCONT = 1024u  // BVH: `cur` is the rest of a leaf whose first primitives were tested (not a new visit)
 };
 
 struct Lane {
@@ -1071,10 +1072,15 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // primitives two more slots; then the wave waits ONCE and each lane computes on the same
 // registers.  Without this a wave with lanes of both kinds paid two dependent round trips per
 // iteration.  Primitives past the second (SAH leaves, bvh.cpp:193) are fetched in pairs after.
-// (Measured alternative, kept out: one primitive per iteration — more iterations, 3 % slower.)
+// LEAF1 (round 3; the path kernels' AA, Whitted, progressive and closest-chain modes, and the
+// streaming kernel): a leaf's primitives one per step instead, through the same four shared loads,
+// so that no load is issued for the few lanes holding a two-primitive leaf — the memory path
+// pays a per-instruction floor (tools/td_lanes.hip): +1.4 % on the headline, +0.4 % on C3, though
+// a leaf takes cnt steps.  (Round 1 measured one primitive per step 3 % slower, before the shared
+// node / leaf fetch.)
 // KIND: 0 = the query kind is the lane's LF_SHADOW flag (path kernels), 1 = closest-hit only,
 // 2 = shadow only (the streaming traversal kernel's specialisations).
-template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, class LaneT>
+template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, bool LEAF1 = true, class LaneT>
 __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kRowBytes;  // desc part; the t part follows
@@ -1085,7 +1091,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   const bool inner = visit && !desc_is_leaf(cur);
   const bool leaf = visit && desc_is_leaf(cur);
   uint32_t first = desc_first(cur), cnt = desc_count(cur);
-  if (leaf && cnt == kBigLeaf) {  // oversized leaf: (first, count) from the side table
+  const bool big = leaf && cnt == kBigLeaf;
+  // LEAF1: one primitive of a leaf per step (below); otherwise the whole leaf in the step
+  const bool whole = !LEAF1 || big;
+  if (big) {  // oversized leaf: (first, count) from the side table
     const uint2 bl = S.big_leaves[first];
     first = bl.x;
     cnt = bl.y;
@@ -1100,7 +1109,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     // only its two child descriptors: the split into two masked loads cost 8.6 %.)
     s3 = rec[3];
   }
-  if (leaf && cnt > 1) {
+  if (leaf && whole && cnt > 1) {
     s4 = rec[4];
     s5 = rec[5];
   }
@@ -1157,7 +1166,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     if (__ballot(leaf) != 0 && (threadIdx.x & 63u) == 0) C.v[ST_WAVE_LEAF_ITERS]++;
   }
   if (leaf) {
-    if (STATS) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
+    if (STATS && !(fl & LF_LEAFCONT)) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
     bool done = false;  // shadow any-hit found (bvh.cpp:376-377)
     // leaf_test: one Object::hit of the leaf in order (bvh.cpp:287-295 / :370-378)
     auto leaf_test = [&](const float4& p0, const float4& p1, const float4& p2, uint32_t prim) {
@@ -1177,9 +1186,9 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       }
     };
     if (cnt > 0) leaf_test(s0, s1, s2, first);
-    if (!done && cnt > 1) leaf_test(s3, s4, s5, first + 1);
+    if (whole && !done && cnt > 1) leaf_test(s3, s4, s5, first + 1);
     const float4* pr = S.prims + 3 * (size_t)first;
-    for (uint32_t i = 2; !done && i < cnt; i += 2) {  // primitives in pairs, tested in order
+    for (uint32_t i = 2; whole && !done && i < cnt; i += 2) {  // primitives in pairs, tested in order
       const bool two = i + 1 < cnt;
       const float4 p0 = pr[3 * i], p1 = pr[3 * i + 1], p2 = pr[3 * i + 2];
       float4 r0, r1, r2;
@@ -1191,7 +1200,14 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       leaf_test(p0, p1, p2, first + i);
       if (!done && two) leaf_test(r0, r1, r2, first + i + 1);
     }
-    if (fl & LF_TRAV) fl |= LF_POP;
+    // A leaf of up to 30 primitives goes on with its next primitive in the next step, whose shared
+    // four loads fetch it with the other lanes' nodes: the rest of the leaf is itself a leaf
+    // descriptor.  (The second primitive's two slots loaded beside the first, for the few lanes
+    // with such a leaf, cost a load instruction each at a per-instruction floor: tools/td_lanes.hip.)
+    const bool more = !whole && !done && cnt > 1;
+    if (more) L.cur = leaf_desc(first + 1, cnt - 1);
+    fl = more ? (fl | LF_LEAFCONT) : (fl & ~LF_LEAFCONT);
+    if (!more && (fl & LF_TRAV)) fl |= LF_POP;
   }
   if (STATS) cyc_leaf += stamp_cycles() - t0;
   if ((fl & (LF_POP | LF_TRAV)) == (LF_POP | LF_TRAV)) {  // bvh.cpp:299-311 / :381-387
@@ -1816,7 +1832,12 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         if (in_trav) grid_step<TRI_ONLY, STATS>(S, L, C, (const LdsU32*)lds_bytes, F.grid_walk, F.grid_pairs);
       } else {
         const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
-        if (in_trav) node_step<TRI_ONLY, STATS, CAP>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
+        // one primitive of a leaf per step (headline +1.4 %, C3 +0.4 %), except in the replay
+        // pass, whose register allocation it tips (VGPR spills 42 -> 96, C4 1 290 -> 770 Mrays/s),
+        // and in one-pass in-order frames (scratch 2 464 -> 2 496 B)
+        constexpr bool kLeaf1 = MODE != MODE_REPLAY && MODE != MODE_SEQ;
+        if (in_trav)
+          node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
       }
     }
     const uint64_t t2 = stamp();
