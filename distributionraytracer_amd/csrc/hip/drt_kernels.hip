@@ -1832,10 +1832,11 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         if (in_trav) grid_step<TRI_ONLY, STATS>(S, L, C, (const LdsU32*)lds_bytes, F.grid_walk, F.grid_pairs);
       } else {
         const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
-        // one primitive of a leaf per step (headline +1.4 %, C3 +0.4 %), except in the replay
-        // pass, whose register allocation it tips (VGPR spills 42 -> 96, C4 1 290 -> 770 Mrays/s),
-        // and in one-pass in-order frames (scratch 2 464 -> 2 496 B)
-        constexpr bool kLeaf1 = MODE != MODE_REPLAY && MODE != MODE_SEQ;
+        // one primitive of a leaf per step (headline +1.4 %, C3 +0.4 %) in triangle scenes, except
+        // in the replay pass, whose register allocation it tips (VGPR spills 42 -> 96, C4 1 290 ->
+        // 770 Mrays/s), and in one-pass in-order frames (scratch 2 464 -> 2 496 B); mixed-primitive
+        // scenes keep the whole-leaf step (C2, balls_low: 23 000 -> 20 800 Mrays/s with it)
+        constexpr bool kLeaf1 = TRI_ONLY && MODE != MODE_REPLAY && MODE != MODE_SEQ;
         if (in_trav)
           node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
       }
