@@ -1080,7 +1080,7 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // node / leaf fetch.)
 // KIND: 0 = the query kind is the lane's LF_SHADOW flag (path kernels), 1 = closest-hit only,
 // 2 = shadow only (the streaming traversal kernel's specialisations).
-template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, bool LEAF1 = true, class LaneT>
+template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, int LEAF1 = 1, class LaneT>
 __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kRowBytes;  // desc part; the t part follows
@@ -1092,8 +1092,9 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   const bool leaf = visit && desc_is_leaf(cur);
   uint32_t first = desc_first(cur), cnt = desc_count(cur);
   const bool big = leaf && cnt == kBigLeaf;
-  // LEAF1: one primitive of a leaf per step (below); otherwise the whole leaf in the step
-  const bool whole = !LEAF1 || big;
+  // LEAF1 1 / 2: one primitive of a leaf per step (below), 2 also leaving the last slot unread for
+  // such a step; 0: the whole leaf in the step
+  const bool whole = LEAF1 == 0 || big;
   if (big) {  // oversized leaf: (first, count) from the side table
     const uint2 bl = S.big_leaves[first];
     first = bl.x;
@@ -1107,7 +1108,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     s2 = rec[2];
     // (Measured alternative, kept out: an 8-B load of the last slot for inner nodes, which use
     // only its two child descriptors: the split into two masked loads cost 8.6 %.)
-    s3 = rec[3];
+    // The last slot serves inner nodes (child descriptors) and whole-leaf steps (the second
+    // primitive's first slot); a one-primitive leaf step does not read it (LEAF1 2: +1.3 % on the
+    // headline; the closest-chain pass of in-order frames lost 1.5 % with it and keeps 1).
+    if (LEAF1 != 2 || inner || whole) s3 = rec[3];
   }
   if (leaf && whole && cnt > 1) {
     s4 = rec[4];
@@ -1836,7 +1840,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         // in the replay pass, whose register allocation it tips (VGPR spills 42 -> 96, C4 1 290 ->
         // 770 Mrays/s), and in one-pass in-order frames (scratch 2 464 -> 2 496 B); mixed-primitive
         // scenes keep the whole-leaf step (C2, balls_low: 23 000 -> 20 800 Mrays/s with it)
-        constexpr bool kLeaf1 = TRI_ONLY && MODE != MODE_REPLAY && MODE != MODE_SEQ;
+        constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL ? 1 : 2);
         if (in_trav)
           node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
       }
