@@ -37,6 +37,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip ta
 # gathers at 6 waves/SIMD), measured by tools/gather_ceiling.hip on one MI355X
 CEILING_JSON = ROOT / "profiles" / "gather_ceiling.json"
 NODE_BYTES, PRIM_BYTES = 64, 48  # one inner-node record (both child boxes), one primitive record
+# shadow tree (drt_layout.hpp): one 4-ary record (four quantised child boxes + descriptors), and the
+# exact leaf-box record an in-range shadow hit is checked against
+WIDE_BYTES, LEAFBOX_BYTES = 64, 32
 CAMERA = dict(eye=(2.1, 1.3, 1.7), at=(0.0, 0.0, 0.0), up=(0.0, 0.0, 1.0), fovy=45.0, hither=0.01)
 FLOOR = np.array([[-4, -4, -1.2, 4, -4, -1.2, 4, 4, -1.2], [-4, -4, -1.2, 4, 4, -1.2, -4, 4, -1.2]], np.float32)
 
@@ -191,6 +194,10 @@ def main():
                          "timed frames ran 3 %% slower than the steady 87.8 ms)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-load-timing", action="store_true",
+                    help="skip the P3F leg: the synthetic scene written as a .p3f file (by a child process "
+                         "while the GPU runs) and parsed + built after the timed region (f1: Scene::load_p3f "
+                         "+ BVH::Build, scene.cpp:565-594, bvh.cpp:27-227)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -225,6 +232,19 @@ def main():
         if rank == 0:
             print(*a, file=sys.stderr, flush=True)
 
+    # f1 leg: the same scene as a P3F file, written by a child process while the GPU works (np.savetxt
+    # of 3M vertices takes ~10 s of one core), parsed and built after the timed region
+    p3f_writer, p3f_path = None, None
+    if rank == 0 and args.scene == "synthetic" and not args.no_load_timing:
+        import subprocess
+        import tempfile
+
+        p3f_path = Path(tempfile.gettempdir()) / f"drt_bench_{os.getpid()}_{args.tris}.p3f"
+        code = ("import sys; sys.path.insert(0, %r); from tests import scenegen as sg; "
+                "sg.write_synthetic_p3f(%r, %d, res=(%d, %d), spp=%d, accel=%r, seed=%d, aperture=%r, focal=%r)"
+                % (str(ROOT), str(p3f_path), args.tris, args.res, args.res, args.spp, args.accel, args.seed,
+                   args.aperture, args.focal))
+        p3f_writer = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.DEVNULL)
     t0 = time.time()
     tris = synthetic_triangles(args.tris, args.seed) if args.scene == "synthetic" else None
     ext = {"aperture": args.aperture, "focal": args.focal, "roughness": args.roughness,
@@ -276,7 +296,8 @@ def main():
     keys = ["closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_prims", "shadow_prims",
             "closest_leaf", "shadow_leaf", "samples", "wave_node_iters", "wave_path_iters", "lane_path_iters",
             "cycles_refill", "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
-            "wave_leaf_iters", "cycles_leaf"]
+            "wave_leaf_iters", "cycles_leaf", "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims",
+            "wide_verify"]
     mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     tot = mine.clone()
     if world > 1:
@@ -353,7 +374,8 @@ def main():
     if kernel_ms is None:
         kernel_ms = serial_ms
     bytes_launch = NODE_BYTES * (mine["closest_inner"] + mine["shadow_inner"]) + \
-        PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"])
+        PRIM_BYTES * (mine["closest_prims"] + mine["shadow_prims"] + mine["wide_prims"]) + \
+        WIDE_BYTES * mine["wide_inner"] + LEAFBOX_BYTES * mine["wide_verify"]
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     ceiling = load_ceiling()
     traffic = None
@@ -445,17 +467,24 @@ def main():
         "msamples_per_s": round(tot["samples"] * args.steps / dt / 1e6, 2),
         "bytes_per_ray": round(bytes_launch / max(1.0, mine["closest_rays"] + mine["shadow_rays"]), 1),
         "node_visits_per_ray": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
-                                      tot["shadow_leaf"]) / max(1.0, rays_frame), 2),
-        "setup_s": round(build_s, 2),
+                                      tot["shadow_leaf"] + tot["wide_inner"] + tot["wide_leaf"]) / max(1.0, rays_frame), 2),
+        # shadow queries on the 4-ary shadow tree: their share and records per query
+        "shadow_tree": {"share": round(tot["wide_shadow_rays"] / max(1.0, tot["shadow_rays"]), 4),
+                        "inner_per_query": round(tot["wide_inner"] / max(1.0, tot["wide_shadow_rays"]), 2),
+                        "leaf_per_query": round(tot["wide_leaf"] / max(1.0, tot["wide_shadow_rays"]), 2),
+                        "prims_per_query": round(tot["wide_prims"] / max(1.0, tot["wide_shadow_rays"]), 2),
+                        "verify_per_query": round(tot["wide_verify"] / max(1.0, tot["wide_shadow_rays"]), 3)},
+        "setup_s": round(build_s, 2),  # scene from in-memory triangles + BVH build (the P3F path: "load")
         # fraction of lanes doing useful work in the node loop / in the path loop (wave64)
         # (Grid: a wave iteration also walks empty cells, several per lane, so visits per wave
         # iteration is not a lane fraction there; tools/grid_diag.py has the Grid's own counters)
         "simd_eff": {"node_loop": round((tot["closest_inner"] + tot["shadow_inner"] + tot["closest_leaf"] +
-                                         tot["shadow_leaf"]) / max(1.0, 64 * tot["wave_node_iters"]), 3)
+                                         tot["shadow_leaf"] + tot["wide_inner"] + tot["wide_leaf"] + tot["wide_verify"])
+                                        / max(1.0, 64 * tot["wave_node_iters"]), 3)
                      if args.accel != "grid" else None,
                      "path_loop": round(tot["lane_path_iters"] / max(1.0, 64 * tot["wave_path_iters"]), 3),
                      # BVH leaf block only (the Grid stepper has no separate leaf block)
-                     "leaf_block": round((tot["closest_leaf"] + tot["shadow_leaf"]) /
+                     "leaf_block": round((tot["closest_leaf"] + tot["shadow_leaf"] + tot["wide_leaf"]) /
                                          (64 * tot["wave_leaf_iters"]), 3) if tot["wave_leaf_iters"] else None},
         # traversal-stack pushes per ray and the share that went past the LDS part (scratch)
         "stack": {"pushes_per_ray": round(tot["stack_pushes"] / max(1.0, rays_frame), 2),
@@ -472,6 +501,27 @@ def main():
                             "leaf_block": round(tot["cycles_leaf"] / max(1.0, tot["wave_leaf_iters"]), 1),
                             "shade": round(tot["cycles_shade"] / max(1.0, tot["wave_path_iters"]), 1)},
     }
+    if p3f_writer is not None:  # f1: Scene::load_p3f + BVH::Build of the file (the reference: 65 s)
+        try:
+            p3f_writer.wait(timeout=300)
+            drt_scene_bytes = p3f_path.stat().st_size
+            t_l = time.perf_counter()
+            fs = drt.Scene.load_p3f(p3f_path)
+            parse_s = time.perf_counter() - t_l
+            t_l = time.perf_counter()
+            fs.build()
+            fbuild_s = time.perf_counter() - t_l
+            same = fs.info().n_objects == info.n_objects and fs.info().bvh_nodes == info.bvh_nodes
+            out["load"] = {"p3f_bytes": drt_scene_bytes, "parse_s": round(parse_s, 2), "build_s": round(fbuild_s, 2),
+                           "load_build_s": round(parse_s + fbuild_s, 2), "same_scene": bool(same),
+                           "note": "setup_s builds from in-memory triangles; this is the P3F file path"}
+            log(f"[bench] P3F {drt_scene_bytes / 1e6:.0f} MB: parse {parse_s:.2f} s, BVH build {fbuild_s:.2f} s")
+            del fs
+        except Exception as e:  # reported, never required
+            out["load"] = {"error": repr(e)}
+            p3f_writer.kill()
+        finally:
+            p3f_path.unlink(missing_ok=True)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
 

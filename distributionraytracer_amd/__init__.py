@@ -18,7 +18,7 @@ from pathlib import Path
 import numpy as np
 
 from . import _lib
-from ._lib import ACCEL, FRAME_STATS, DrtCamera, DrtFrameParams, DrtFrameStats, DrtOptions, DrtSceneInfo, check
+from ._lib import ACCEL, FRAME_REFERENCE_ORDER, FRAME_STATS, DrtCamera, DrtFrameParams, DrtFrameStats, DrtOptions, DrtSceneInfo, check
 
 __all__ = ["Scene", "Renderer", "RendererGroup", "ACCEL", "load_skybox_dir", "SKY_FACES", "build"]
 
@@ -268,7 +268,7 @@ class Renderer:
         return self
 
     def frame_params(self, seed=1, max_depth=4, roughness=0.0, shard=0, n_shards=1, tile=16, stats=False,
-                     light_spp=1, progressive_frame=0, slot=0):
+                     light_spp=1, progressive_frame=0, slot=0, reference_order=False):
         p = DrtFrameParams()
         p.slot = slot
         p.light_spp = light_spp
@@ -279,13 +279,15 @@ class Renderer:
         p.shard = shard
         p.n_shards = n_shards
         p.tile = tile
-        p.flags = FRAME_STATS if stats else 0
+        p.flags = (FRAME_STATS if stats else 0) | (FRAME_REFERENCE_ORDER if reference_order else 0)
         return p
 
     def render(self, seed=1, max_depth=4, roughness=0.0, stats=False, tile=16, light_spp=1, progressive_frame=0,
-               accum=None):
+               accum=None, reference_order=False):
         """Whole frame to host memory.  progressive_frame n >= 1: zone A frame n lerped into
-        `accum` (updated in place and returned)."""
+        `accum` (updated in place and returned).  reference_order: shadow queries walk the
+        reference's binary tree in its visit order (DRT_FRAME_REFERENCE_ORDER), so stats() counts
+        the reference's shadow work; the frame is the same either way."""
         info = self.scene.info()
         if accum is not None:
             if accum.dtype != np.float32 or accum.shape != (info.res_y, info.res_x, 3) or not accum.flags.c_contiguous:
@@ -294,7 +296,7 @@ class Renderer:
         else:
             out = np.zeros((info.res_y, info.res_x, 3), np.float32)
         p = self.frame_params(seed, max_depth, roughness, tile=tile, stats=stats, light_spp=light_spp,
-                              progressive_frame=progressive_frame)
+                              progressive_frame=progressive_frame, reference_order=reference_order)
         check(_lib.load().drt_render(self.h, C.byref(p), _fp(out)), self.h, "drt_render")
         return out
 
@@ -368,9 +370,11 @@ class Renderer:
         check(_lib.load().drt_trace_device(self.h, int(bool(shadow)), v(d_rays), int(n), v(d_t), v(d_normal),
                                            v(d_object), v(d_occluded), v(stream or 0)), self.h, "drt_trace_device")
 
-    def set_trace_stats(self, on=True):
-        """Count traversal work (rays, nodes, leaves, primitives) of later batched queries."""
-        check(_lib.load().drt_set_trace_flags(self.h, FRAME_STATS if on else 0), self.h, "drt_set_trace_flags")
+    def set_trace_stats(self, on=True, reference_order=False):
+        """Count traversal work (rays, nodes, leaves, primitives) of later batched queries;
+        reference_order: later shadow queries walk the reference's binary tree."""
+        flags = (FRAME_STATS if on else 0) | (FRAME_REFERENCE_ORDER if reference_order else 0)
+        check(_lib.load().drt_set_trace_flags(self.h, flags), self.h, "drt_set_trace_flags")
 
     def trace_stats(self):
         """Streaming-kernel time (kernel_ms) and counters of the last BVH batched query."""

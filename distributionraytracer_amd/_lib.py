@@ -20,6 +20,7 @@ STATUS = {0: "DRT_OK", -1: "DRT_E_INVALID", -2: "DRT_E_HIP", -3: "DRT_E_NODEVICE
           -5: "DRT_E_STATE", -6: "DRT_E_UNSUPPORTED"}
 ACCEL = {"none": 0, "grid": 1, "bvh": 2}
 FRAME_STATS = 1
+FRAME_REFERENCE_ORDER = 4  # shadow queries on the reference's binary tree, in its visit order
 
 _f = C.POINTER(C.c_float)
 _u8 = C.POINTER(C.c_uint8)
@@ -52,7 +53,8 @@ class DrtFrameStats(C.Structure):
         [(n, C.c_uint64) for n in ("wave_node_iters", "wave_path_iters", "lane_path_iters", "cycles_refill",
                                    "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
                                    "wave_leaf_iters", "cycles_leaf", "seq_pushed", "seq_popped")] + \
-        [("seq_handover", C.c_int32), ("reserved", C.c_int32 * 3)]
+        [("seq_handover", C.c_int32), ("reserved", C.c_int32)] + \
+        [(n, C.c_uint64) for n in ("wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify")]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_

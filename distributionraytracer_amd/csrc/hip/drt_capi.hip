@@ -84,6 +84,11 @@ struct drt_ctx {
   float root_box[6] = {0};
   uint32_t root_desc = 0;
   int bvh_depth = 0;
+  // 4-ary shadow tree collapsed from the BVH (drt_layout.hpp); absent for a leaf root, a tree too
+  // deep for the shadow stack, coordinates no record can quantise, or DRT_WIDE_SHADOW=0
+  bool has_wide = false;
+  DevBuf d_wnodes, d_wleaf;
+  uint32_t wroot = 0, n_wide = 0;
   // grid
   bool has_grid = false;
   int gdim[3] = {0, 0, 0};
@@ -178,6 +183,128 @@ static PrimRecord pack_prim(const drt_prim& p, uint32_t mat, uint32_t obj) {
       break;
   }
   return r;
+}
+
+// ---- 4-ary shadow tree (drt_layout.hpp) -------------------------------------------------------
+// One axis of a wide node: the coarsest-needed power-of-two scale s = 2^E and anchor p = k * s such
+// that every child's [lo, hi] is covered by [p + ql * s, p + qh * s] with 0 <= ql, qh <= 255 and
+// every such plane an exact float (|k| + 255 < 2^24).  False if no exponent fits (non-finite or
+// enormous coordinates): the scene then keeps the binary tree for its shadow queries.
+static bool quantize_axis(const double* lo, const double* hi, int n, float& p, uint32_t& ebits, uint32_t& qlo,
+                          uint32_t& qhi) {
+  double nlo = lo[0], nhi = hi[0];
+  for (int k = 1; k < n; k++) {
+    nlo = std::min(nlo, lo[k]);
+    nhi = std::max(nhi, hi[k]);
+  }
+  if (!std::isfinite(nlo) || !std::isfinite(nhi) || nhi < nlo) return false;
+  int e0 = -126;
+  if (nhi > nlo) e0 = std::max(-126, std::ilogb((nhi - nlo) / 255.0) - 1);
+  for (int E = e0; E <= 120; E++) {
+    const double s = std::ldexp(1.0, E);
+    const double k0 = std::floor(nlo / s);
+    if (std::fabs(k0) + 256.0 >= 16777216.0) continue;
+    uint32_t L = 0, H = 0;
+    bool ok = true;
+    const float pf = (float)(k0 * s), sf = (float)s;
+    if ((double)pf != k0 * s) continue;
+    for (int k = 0; k < 4 && ok; k++) {
+      if (k >= n) {  // unused slot: an inverted box (lo 255 > hi 0)
+        L |= 255u << (8 * k);
+        continue;
+      }
+      const double ql = std::floor(lo[k] / s) - k0, qh = std::ceil(hi[k] / s) - k0;
+      if (ql < 0.0 || qh > 255.0) {
+        ok = false;
+        break;
+      }
+      // the device decodes with one FMA; every value here is exact, so check it as the device does
+      const float dl = std::fma((float)ql, sf, pf), dh = std::fma((float)qh, sf, pf);
+      if (!((double)dl <= lo[k]) || !((double)dh >= hi[k]) || !std::isfinite(dl) || !std::isfinite(dh)) {
+        ok = false;
+        break;
+      }
+      L |= (uint32_t)ql << (8 * k);
+      H |= (uint32_t)qh << (8 * k);
+    }
+    if (!ok) continue;
+    p = pf;
+    ebits = (uint32_t)(E + 127);
+    qlo = L;
+    qhi = H;
+    return true;
+  }
+  return false;
+}
+
+// Collapse the reference's binary tree (nodes, leaf descriptors per node) into 4-ary records: a
+// wide node's children are its binary node's two children, the inner one with the largest box
+// surface replaced by its two children until there are four (or only leaves).  Records in depth-
+// first order.  False if a record cannot be quantised or 3 * depth would overflow the shadow stack.
+static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& leaf_descs,
+                       std::vector<WideNodeRecord>& out, uint32_t& root) {
+  out.clear();
+  if (nodes[0].leaf) return false;
+  auto area = [&](uint32_t i) {
+    const drt_bvh_node& nd = nodes[i];
+    const double x = (double)nd.bmax[0] - nd.bmin[0], y = (double)nd.bmax[1] - nd.bmin[1],
+                 z = (double)nd.bmax[2] - nd.bmin[2];
+    return x * y + y * z + z * x;
+  };
+  struct Item {
+    uint32_t node, slot;
+    int depth;
+  };
+  std::vector<Item> st{{0u, 0u, 1}};
+  out.emplace_back();
+  int maxd = 1;
+  while (!st.empty()) {
+    const Item it = st.back();
+    st.pop_back();
+    maxd = std::max(maxd, it.depth);
+    uint32_t ch[4];
+    int n = 2;
+    ch[0] = nodes[it.node].index;
+    ch[1] = ch[0] + 1;
+    while (n < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (int k = 0; k < n; k++)
+        if (!nodes[ch[k]].leaf && area(ch[k]) > ba) {
+          ba = area(ch[k]);
+          best = k;
+        }
+      if (best < 0) break;
+      const uint32_t c = ch[best];
+      ch[best] = nodes[c].index;
+      ch[n++] = nodes[c].index + 1;
+    }
+    WideNodeRecord r{};
+    for (int a = 0; a < 3; a++) {
+      double lo[4], hi[4];
+      for (int k = 0; k < n; k++) {
+        lo[k] = nodes[ch[k]].bmin[a];
+        hi[k] = nodes[ch[k]].bmax[a];
+      }
+      uint32_t e = 0;
+      if (!quantize_axis(lo, hi, n, r.p[a], e, r.q[2 * a], r.q[2 * a + 1])) return false;
+      r.ebits |= e << (8 * a);
+    }
+    // children pushed in reverse so the first child's subtree follows its parent in memory
+    for (int k = n - 1; k >= 0; k--) {
+      if (nodes[ch[k]].leaf) {
+        r.desc[k] = leaf_descs[ch[k]];
+      } else {
+        r.desc[k] = (uint32_t)out.size();
+        out.emplace_back();
+        st.push_back({ch[k], r.desc[k], it.depth + 1});
+      }
+    }
+    out[it.slot] = r;
+  }
+  if (3 * maxd > kWideMaxStack) return false;
+  root = 0;
+  return true;
 }
 
 extern "C" {
@@ -319,6 +446,11 @@ int drt_set_camera(drt_ctx* c, const drt_camera* k) {
   if (!c || !k) return DRT_E_INVALID;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "set the camera of an uploaded scene");
   if (k->res_x <= 0 || k->res_y <= 0) DRT_FAIL(c, DRT_E_INVALID, "camera resolution must be positive");
+  // Camera::SetEye moves the eye and keeps the resolution (camera.h:63-72); the caller's frame
+  // buffers are sized by it, so a different one is refused (re-upload the scene to change it)
+  if (k->res_x != c->cam.res_x || k->res_y != c->cam.res_y)
+    DRT_FAIL(c, DRT_E_INVALID, "camera resolution %dx%d differs from the resident %dx%d", k->res_x, k->res_y,
+             c->cam.res_x, c->cam.res_y);
   // the frame reaches the kernels by value (SceneArgs, copied at launch): frames already issued
   // keep the camera they were launched with
   c->cam = *k;
@@ -425,6 +557,8 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
     big.push_back(make_uint2(nd.index, nd.n_objs));
     return leaf_desc((uint32_t)big.size() - 1, kBigLeaf);
   };
+  std::vector<uint32_t> dsc(n_nodes);  // every node's descriptor, once (big leaves get one table entry)
+  for (uint32_t i = 0; i < n_nodes; i++) dsc[i] = desc_of(i);
   std::vector<NodeRecord> recs(n_slots);  // padding slots stay zero (never referenced)
   for (uint32_t i = 0; i < n_nodes; i++) {
     if (nodes[i].leaf) continue;
@@ -434,9 +568,25 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
     const float b[12] = {L.bmin[0], L.bmin[1], L.bmin[2], L.bmax[0], L.bmax[1], L.bmax[2],
                          R.bmin[0], R.bmin[1], R.bmin[2], R.bmax[0], R.bmax[1], R.bmax[2]};
     memcpy(r.box, b, sizeof(b));
-    r.desc[0] = desc_of(nodes[i].index);
-    r.desc[1] = desc_of(nodes[i].index + 1);
+    r.desc[0] = dsc[nodes[i].index];
+    r.desc[1] = dsc[nodes[i].index + 1];
     r.desc[2] = r.desc[3] = 0;
+  }
+  // 4-ary shadow tree and the exact reference leaf box of every primitive (DRT_WIDE_SHADOW=0: none)
+  std::vector<WideNodeRecord> wide;
+  uint32_t wroot = 0;
+  const bool has_wide = env_int("DRT_WIDE_SHADOW", 1) != 0 && build_wide(nodes, dsc, wide, wroot);
+  std::vector<LeafBoxRecord> lbox;
+  if (has_wide) {
+    lbox.assign((size_t)n_obj + 2, LeafBoxRecord{});  // + 2: the node step's tail slot reads
+    for (uint32_t i = 0; i < n_nodes; i++) {
+      const drt_bvh_node& nd = nodes[i];
+      if (!nd.leaf) continue;
+      LeafBoxRecord b{};
+      memcpy(b.box, nd.bmin, 12);
+      memcpy(b.box + 3, nd.bmax, 12);
+      for (uint32_t k = 0; k < nd.n_objs; k++) lbox[nd.index + k] = b;
+    }
   }
   // depth (= bound on the traversal stack), iterative
   int maxd = 0;
@@ -456,10 +606,20 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
   c->bvh_depth = maxd;
   memcpy(c->root_box, nodes[0].bmin, 3 * sizeof(float));
   memcpy(c->root_box + 3, nodes[0].bmax, 3 * sizeof(float));
-  c->root_desc = desc_of(0);
+  c->root_desc = dsc[0];
   DRT_HIP(c, hipSetDevice(c->device));
   DRT_HIP(c, c->d_nodes.ensure(sizeof(NodeRecord) * std::max<size_t>(1, recs.size())));
   if (!recs.empty()) DRT_HIP(c, hipMemcpy(c->d_nodes.p, recs.data(), sizeof(NodeRecord) * recs.size(), hipMemcpyHostToDevice));
+  c->has_wide = false;
+  if (has_wide) {
+    DRT_HIP(c, c->d_wnodes.ensure(sizeof(WideNodeRecord) * wide.size()));
+    DRT_HIP(c, hipMemcpy(c->d_wnodes.p, wide.data(), sizeof(WideNodeRecord) * wide.size(), hipMemcpyHostToDevice));
+    DRT_HIP(c, c->d_wleaf.ensure(sizeof(LeafBoxRecord) * lbox.size()));
+    DRT_HIP(c, hipMemcpy(c->d_wleaf.p, lbox.data(), sizeof(LeafBoxRecord) * lbox.size(), hipMemcpyHostToDevice));
+    c->wroot = wroot;
+    c->n_wide = (uint32_t)wide.size();
+    c->has_wide = true;
+  }
   DRT_HIP(c, c->d_big.ensure(sizeof(uint2) * std::max<size_t>(1, big.size())));
   if (!big.empty()) DRT_HIP(c, hipMemcpy(c->d_big.p, big.data(), sizeof(uint2) * big.size(), hipMemcpyHostToDevice));
   // primitive records in BVH object order: every leaf is one contiguous run
@@ -547,7 +707,9 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
 
 }  // extern "C"
 
-static int scene_args(drt_ctx* c, int accel, SceneArgs& S) {
+// reference_order: every shadow query walks the reference's binary tree in its visit order
+// (DRT_FRAME_REFERENCE_ORDER: node / leaf / primitive counts equal the reference's)
+static int scene_args(drt_ctx* c, int accel, SceneArgs& S, bool reference_order) {
   memset(&S, 0, sizeof(S));
   const drt_camera& k = c->cam;
   memcpy(S.eye, k.eye, 12); memcpy(S.u, k.u, 12); memcpy(S.v, k.v, 12); memcpy(S.n, k.n, 12);
@@ -571,6 +733,11 @@ static int scene_args(drt_ctx* c, int accel, SceneArgs& S) {
     S.nodes = c->d_nodes.as<float4>();
     memcpy(S.root_box, c->root_box, sizeof(S.root_box));
     S.root_desc = c->root_desc;
+    if (c->has_wide && !reference_order) {
+      S.wnodes = c->d_wnodes.as<float4>();
+      S.wleaf = c->d_wleaf.as<float4>();
+      S.wroot = c->wroot;
+    }
   } else if (accel == ACC_GRID) {
     if (!c->has_grid) DRT_FAIL(c, DRT_E_STATE, "scene uses a grid but none was uploaded");
     memcpy(S.gdim, c->gdim, sizeof(S.gdim));
@@ -702,7 +869,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   if (rc) return rc;
   if (P.skip) return DRT_OK;
   SceneArgs S;
-  rc = scene_args(c, c->accel, S);
+  rc = scene_args(c, c->accel, S, (p->flags & DRT_FRAME_REFERENCE_ORDER) != 0);
   if (rc) return rc;
   DRT_HIP(c, hipSetDevice(c->device));
   // frames on different scratch slots may run concurrently on different streams
@@ -715,6 +882,17 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // that frame to end (on the device).  Frames of one stream are ordered by the stream itself.
   if (c->slot_used[slot] && c->slot_stream[slot] != st && c->frames - c->slot_frame[slot] < drt_ctx::kRing)
     DRT_HIP(c, hipStreamWaitEvent(st, c->ring[3 * (c->slot_frame[slot] % drt_ctx::kRing) + 2], 0));
+  // Two-pass in-order frame: its closest-hit record is allocated first; a frame whose record does not
+  // fit in device memory runs as the one-pass MODE_SEQ frame, which renders the same pixels.
+  if (P.F.n_items && P.two_pass) {
+    if (c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess ||
+        c->d_skel_hits_s[slot].ensure(sizeof(uint2) * P.n_slots * (uint64_t)(P.F.max_depth + 1)) != hipSuccess) {
+      (void)hipGetLastError();
+      c->d_skel_rk_s[slot].release();
+      c->d_skel_hits_s[slot].release();
+      P.two_pass = false;
+    }
+  }
   // MODE_SEQ tail hand-over (DRT_SEQ_DONATE: 0 off, 1 on, default auto).  It frees whole blocks
   // at the frame's tail for the NEXT frame's blocks, but makes a frame alone slower (a handed-over
   // pixel waits for a lane of a kept wave: C4 820-828 -> 853-902 ms).  Auto turns it
@@ -803,10 +981,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     }  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
   if (P.F.n_items && P.two_pass) {
-    DevBuf& d_rk = c->d_skel_rk_s[slot];
+    DevBuf& d_rk = c->d_skel_rk_s[slot];  // allocated above
     DevBuf& d_hits = c->d_skel_hits_s[slot];
-    DRT_HIP(c, d_rk.ensure(sizeof(uint32_t) * P.n_slots));
-    DRT_HIP(c, d_hits.ensure(sizeof(uint2) * P.n_slots * (uint64_t)(P.F.max_depth + 1)));
     FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order
     F1.mode = MODE_SKEL;
     F1.skel_rk = d_rk.as<uint32_t>();
@@ -985,6 +1161,11 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.stack_spills = s[ST_PUSH_SPILL];
       c->last.wave_leaf_iters = s[ST_WAVE_LEAF_ITERS];
       c->last.cycles_leaf = s[ST_CYC_LEAF];
+      c->last.wide_shadow_rays = s[ST_W_RAYS];
+      c->last.wide_inner = s[ST_W_INNER];
+      c->last.wide_leaf = s[ST_W_LEAF];
+      c->last.wide_prims = s[ST_W_PRIMS];
+      c->last.wide_verify = s[ST_W_VERIFY];
     }
     c->last.seq_handover = c->slot_handover[c->stats_slot] ? 1 : 0;
     if (c->last.seq_handover) {  // push / pop counts of the frame's continuation slots
@@ -1005,7 +1186,7 @@ static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, 
                         uint8_t* docc, hipStream_t st) {
   SceneArgs S;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
-  int rc = scene_args(c, c->accel, S);
+  int rc = scene_args(c, c->accel, S, (c->trace_flags & DRT_FRAME_REFERENCE_ORDER) != 0);
   if (rc) return rc;
   DRT_HIP(c, hipSetDevice(c->device));
   c->trace_timed = false;
@@ -1115,6 +1296,11 @@ int drt_trace_stats(drt_ctx* c, drt_frame_stats* out) {
       r.stack_pushes = s[ST_PUSH];
       r.stack_spills = s[ST_PUSH_SPILL];
       r.wave_leaf_iters = s[ST_WAVE_LEAF_ITERS];
+      r.wide_shadow_rays = s[ST_W_RAYS];
+      r.wide_inner = s[ST_W_INNER];
+      r.wide_leaf = s[ST_W_LEAF];
+      r.wide_prims = s[ST_W_PRIMS];
+      r.wide_verify = s[ST_W_VERIFY];
     }
   }
   *out = r;

@@ -188,6 +188,17 @@ drt_ctx* drt_group_ctx(drt_group* g, int rank) { return (g && rank >= 0 && rank 
 
 int drt_group_set_camera(drt_group* g, const drt_camera* camera) {
   if (!g || !camera) return DRT_E_INVALID;
+  // validated once for every device before any device changes, so that a refusal leaves every
+  // device on the old camera (a group frame never mixes tiles of two cameras); drt_set_camera's
+  // checks are these
+  if (camera->res_x <= 0 || camera->res_y <= 0) G_FAIL(g, DRT_E_INVALID, "camera resolution must be positive");
+  for (int r = 0; r < g->n; r++) {
+    int32_t res[2] = {0, 0};
+    if (drt_frame_resolution(g->ctx[r], res) != DRT_OK) G_FAIL(g, DRT_E_STATE, "device %d: no scene uploaded", g->dev[r]);
+    if (res[0] != camera->res_x || res[1] != camera->res_y)
+      G_FAIL(g, DRT_E_INVALID, "device %d: camera resolution %dx%d differs from the resident %dx%d", g->dev[r],
+             camera->res_x, camera->res_y, res[0], res[1]);
+  }
   for (int r = 0; r < g->n; r++) {
     const int rc = drt_set_camera(g->ctx[r], camera);
     if (rc) G_FAIL(g, rc, "device %d: %s", g->dev[r], drt_last_error(g->ctx[r]));

@@ -753,7 +753,9 @@ enum LaneFlag : uint32_t {
   LF_INCELL = 128u, // Grid: objects of the current cell left, from record L.spa on
   LF_YIELD = 256u,  // MODE_SEQ tail: the lane's wave is handing its pixels over (set per shading pass)
   LF_RESUME = 512u, // MODE_SEQ tail: the lane took over a pixel; its next sample starts in finish_sample
-  LF_LEAFCONT = 1024u  // BVH: `cur` is the rest of a leaf whose first primitives were tested (not a new visit)
+  LF_LEAFCONT = 1024u, // BVH: `cur` is the rest of a leaf whose first primitives were tested (not a new visit)
+  LF_WIDE = 2048u,     // BVH shadow query on the 4-ary shadow tree (drt_layout.hpp)
+  LF_VERIFY = 4096u    // shadow tree: primitive `cur` was hit within range; check its leaf's exact box
 };
 
 struct Lane {
@@ -1031,7 +1033,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   L.fl = fl;
 }
 
-template <bool STATS, int ACC>
+template <bool STATS, int ACC, bool WIDE = false>
 __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const RayP& q, bool shadow, float thr,
                                             Counters& C) {
   if (STATS) C.v[shadow ? ST_SHADOW : ST_CLOSEST]++;
@@ -1050,7 +1052,15 @@ __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const R
   float tmp;
   const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
                             S.root_box[5], q, tmp);  // bvh.cpp:242 / :328: a root miss is an empty result
-  L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (ray_finite(q) ? LF_FINITE : 0u);
+  const bool fin = ray_finite(q);
+  L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (fin ? LF_FINITE : 0u);
+  // finite shadow rays walk the 4-ary shadow tree; the others keep the reference's slab NaN rules
+  // on its binary tree
+  if (WIDE && shadow && fin && S.wnodes != nullptr) {
+    if (STATS) C.v[ST_W_RAYS]++;
+    L.fl |= LF_WIDE;
+    L.cur = S.wroot;
+  }
 }
 
 __device__ __forceinline__ uint64_t stamp_cycles() {
@@ -1080,16 +1090,24 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // node / leaf fetch.)
 // KIND: 0 = the query kind is the lane's LF_SHADOW flag (path kernels), 1 = closest-hit only,
 // 2 = shadow only (the streaming traversal kernel's specialisations).
-template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, int LEAF1 = 1, class LaneT>
+// WIDE (path kernels with shadow queries, the streaming shadow kernel): lanes flagged LF_WIDE walk
+// the 4-ary shadow tree (drt_layout.hpp) — a wide record in the same four shared slot loads, its
+// four child boxes tested at once, the nearest hit child next and the others pushed — and an
+// in-range primitive hit becomes LF_VERIFY: the next step loads that primitive's exact reference
+// leaf box through the same shared loads and accepts the hit only if the box is hit
+// (boundingBox.cpp:64-124), else the leaf is dropped and the walk goes on.
+template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, int LEAF1 = 1, bool WIDE = false, class LaneT>
 __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kRowBytes;  // desc part; the t part follows
   uint32_t fl = L.fl;
   const bool shadow = KIND == 0 ? (fl & LF_SHADOW) != 0u : KIND == 2;
+  const bool wide = WIDE && (fl & LF_WIDE) != 0u;
   const uint32_t cur = L.cur;
   const bool visit = !(fl & LF_POP);
-  const bool inner = visit && !desc_is_leaf(cur);
-  const bool leaf = visit && desc_is_leaf(cur);
+  const bool verify = WIDE && visit && (fl & LF_VERIFY) != 0u;
+  const bool inner = visit && !verify && !desc_is_leaf(cur);
+  const bool leaf = visit && !verify && desc_is_leaf(cur);
   uint32_t first = desc_first(cur), cnt = desc_count(cur);
   const bool big = leaf && cnt == kBigLeaf;
   // LEAF1 1 / 2: one primitive of a leaf per step (below), 2 also leaving the last slot unread for
@@ -1100,7 +1118,8 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     first = bl.x;
     cnt = bl.y;
   }
-  const float4* rec = leaf ? S.prims + 3 * (size_t)first : S.nodes + 4 * (size_t)cur;
+  const float4* rec = leaf ? S.prims + 3 * (size_t)first
+                           : (verify ? S.wleaf + 2 * (size_t)cur : (wide ? S.wnodes : S.nodes) + 4 * (size_t)cur);
   float4 s0, s1, s2, s3, s4, s5;
   if (visit) {
     s0 = rec[0];
@@ -1123,7 +1142,72 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   // an L1-resident table in isolation, but the path kernel ran 1 068 against 1 736 Mrays/s and the
   // streaming traversal kernel 0.65-0.78x: the transpose's ~50 VALU and DPP hazards sit on each
   // step's load -> test -> next-address chain, and the step must run with the whole wave active.)
-  if (inner) {
+  if (WIDE && inner && wide) {
+    if (STATS) C.v[ST_W_INNER]++;
+    // Child boxes decoded exactly (p + q * 2^E is a float, drt_layout.hpp) and tested with the
+    // reference's sign-selected slabs (boundingBox.cpp:69-101; the ray is finite): each decoded box
+    // contains the child's reference box, and the slab values are monotone in the planes, so a ray
+    // that hits a reference box hits its decoded box.  The near / far plane bytes of all four
+    // children are selected per axis at once.
+    const uint32_t eb = __float_as_uint(s0.w);
+    const float scx = __uint_as_float((eb & 0xffu) << 23), scy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
+                scz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
+    const uint32_t lx = __float_as_uint(s1.x), hx = __float_as_uint(s1.y), ly = __float_as_uint(s1.z),
+                   hy = __float_as_uint(s1.w), lz = __float_as_uint(s2.x), hz = __float_as_uint(s2.y);
+    const bool px = L.q.sx(), py = L.q.sy(), pz = L.q.sz();
+    const uint32_t nx = px ? lx : hx, fx = px ? hx : lx, ny = py ? ly : hy, fy = py ? hy : ly, nz = pz ? lz : hz,
+                   fz = pz ? hz : lz;
+    const uint32_t d[4] = {__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w)};
+    float tn[4];
+    bool hk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int sh = 8 * k;
+      const float tnx = (__builtin_fmaf((float)((nx >> sh) & 0xffu), scx, s0.x) - L.q.o.x) * L.q.ix;
+      const float tfx = (__builtin_fmaf((float)((fx >> sh) & 0xffu), scx, s0.x) - L.q.o.x) * L.q.ix;
+      const float tny = (__builtin_fmaf((float)((ny >> sh) & 0xffu), scy, s0.y) - L.q.o.y) * L.q.iy;
+      const float tfy = (__builtin_fmaf((float)((fy >> sh) & 0xffu), scy, s0.y) - L.q.o.y) * L.q.iy;
+      const float tnz = (__builtin_fmaf((float)((nz >> sh) & 0xffu), scz, s0.z) - L.q.o.z) * L.q.iz;
+      const float tfz = (__builtin_fmaf((float)((fz >> sh) & 0xffu), scz, s0.z) - L.q.o.z) * L.q.iz;
+      const float t0 = fmaxf(fmaxf(tnx, tny), tnz), t1 = fminf(fminf(tfx, tfy), tfz);
+      hk[k] = fmaxf(t0, 0.0f) < t1;  // t0 < t1 && t1 > 0
+      tn[k] = t0;
+    }
+    // go on with the hit child entered first (any order gives the same answer); push the others
+    int ci = -1;
+    float best = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool take = hk[k] && (ci < 0 || tn[k] < best);
+      ci = take ? k : ci;
+      best = take ? tn[k] : best;
+    }
+    constexpr uint32_t kWideLds = 2u * kLdsBytes;  // a shadow-tree stack uses the t rows too
+    uint32_t spa = L.spa;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (hk[k] && k != ci) {
+        if (spa < kWideLds) *(LdsU32*)(lds + spa) = d[k];
+        else ov_desc[(spa - kWideLds) >> kRowShift] = d[k];
+        if (STATS) {
+          C.v[ST_PUSH]++;
+          if (spa >= kWideLds) C.v[ST_PUSH_SPILL]++;
+        }
+        spa += kRowBytes;
+      }
+    }
+    L.spa = spa;
+    L.cur = ci == 0 ? d[0] : (ci == 1 ? d[1] : (ci == 2 ? d[2] : d[3]));
+    fl |= ci < 0 ? LF_POP : 0u;
+  }
+  if (WIDE && verify) {  // the exact reference leaf box of primitive `cur`, hit within range
+    if (STATS) C.v[ST_W_VERIFY]++;
+    float tv;
+    const bool in = box_test_finite(s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, L.q, tv);
+    fl &= ~LF_VERIFY;
+    fl = in ? ((fl | LF_HIT) & ~LF_TRAV) : (fl | LF_POP);
+  }
+  if (inner && !wide) {
     if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
     const float4 a = s0, b = s1, c = s2;
     const uint4 d = make_uint4(__float_as_uint(s3.x), __float_as_uint(s3.y), 0u, 0u);
@@ -1170,16 +1254,22 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     if (__ballot(leaf) != 0 && (threadIdx.x & 63u) == 0) C.v[ST_WAVE_LEAF_ITERS]++;
   }
   if (leaf) {
-    if (STATS && !(fl & LF_LEAFCONT)) C.v[shadow ? ST_S_LEAF : ST_C_LEAF]++;
+    if (STATS && !(fl & LF_LEAFCONT)) C.v[wide ? ST_W_LEAF : (shadow ? ST_S_LEAF : ST_C_LEAF)]++;
     bool done = false;  // shadow any-hit found (bvh.cpp:376-377)
     // leaf_test: one Object::hit of the leaf in order (bvh.cpp:287-295 / :370-378)
     auto leaf_test = [&](const float4& p0, const float4& p1, const float4& p2, uint32_t prim) {
-      if (STATS) C.v[shadow ? ST_S_PRIMS : ST_C_PRIMS]++;
+      if (STATS) C.v[wide ? ST_W_PRIMS : (shadow ? ST_S_PRIMS : ST_C_PRIMS)]++;
       float t;
       if (hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t)) {
         if (shadow) {
           if (t <= L.thr) {
-            fl = (fl | LF_HIT) & ~LF_TRAV;
+            // shadow tree: the leaf was entered through a containing box; its exact box decides
+            if (wide) {
+              fl |= LF_VERIFY;
+              L.cur = prim;
+            } else {
+              fl = (fl | LF_HIT) & ~LF_TRAV;
+            }
             done = true;
           }
         } else if (t < L.best_t) {
@@ -1211,7 +1301,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     const bool more = !whole && !done && cnt > 1;
     if (more) L.cur = leaf_desc(first + 1, cnt - 1);
     fl = more ? (fl | LF_LEAFCONT) : (fl & ~LF_LEAFCONT);
-    if (!more && (fl & LF_TRAV)) fl |= LF_POP;
+    if (!more && (fl & LF_TRAV) && !(WIDE && (fl & LF_VERIFY))) fl |= LF_POP;
   }
   if (STATS) cyc_leaf += stamp_cycles() - t0;
   if ((fl & (LF_POP | LF_TRAV)) == (LF_POP | LF_TRAV)) {  // bvh.cpp:299-311 / :381-387
@@ -1221,13 +1311,15 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       const uint32_t spa = L.spa - kRowBytes;
       L.spa = spa;
       uint32_t pd;
-      float pt;
-      if (spa < kLdsBytes) {
+      float pt = 0.0f;
+      // a shadow-tree lane's LDS stack spans the t rows too (it keeps no entry distances)
+      const uint32_t lim = wide ? 2u * kLdsBytes : kLdsBytes;
+      if (spa < lim) {
         pd = *(LdsU32*)(lds + spa);
-        pt = *(LdsF32*)(lds + kLdsBytes + spa);
+        if (!shadow) pt = *(LdsF32*)(lds + kLdsBytes + spa);
       } else {
-        pd = ov_desc[(spa >> kRowShift) - CAP];
-        pt = ov_t[(spa >> kRowShift) - CAP];
+        pd = ov_desc[(spa - lim) >> kRowShift];
+        pt = ov_t[(spa - lim) >> kRowShift];
       }
       if (shadow || pt < L.best_t) {
         L.cur = pd;
@@ -1253,7 +1345,7 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
   if (ACC == ACC_GRID)  // Grid::Traverse(Ray&) gets the unit L: range |L|, direction re-normalised (Q1)
     start_query<STATS, ACC>(S, L, make_ray(so, normalize(Lv)), true, length(Lv), C);
   else  // BVH::Traverse(Ray&) normalises Ls and accepts t <= |Ls| + EPSILON (bvh.cpp:321-322, :376)
-    start_query<STATS, ACC>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
+    start_query<STATS, ACC, true>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
 }
 
 // reflectDir (main.cpp:504-508); MODE_SEQ draws rnd_unit_sphere on the lane's keyed stream
@@ -1841,8 +1933,11 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         // 770 Mrays/s), and in one-pass in-order frames (scratch 2 464 -> 2 496 B); mixed-primitive
         // scenes keep the whole-leaf step (C2, balls_low: 23 000 -> 20 800 Mrays/s with it)
         constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL ? 1 : 2);
+        // every mode with shadow queries walks them on the shadow tree (the closest-chain pass has none)
+        constexpr bool kWide = MODE != MODE_SKEL;
         if (in_trav)
-          node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc[3]);
+          node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1, kWide>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C,
+                                                            cyc[3]);
       }
     }
     const uint64_t t2 = stamp();
@@ -1944,8 +2039,14 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
           float tmp;
           const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
                                     S.root_box[5], L.q, tmp);  // bvh.cpp:242 / :328
-          L.fl = (KIND == 2 ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (ray_finite(L.q) ? LF_FINITE : 0u);
+          const bool fin = ray_finite(L.q);
+          L.fl = (KIND == 2 ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (fin ? LF_FINITE : 0u);
           if (STATS) C.v[KIND == 2 ? ST_SHADOW : ST_CLOSEST]++;
+          if (KIND == 2 && fin && S.wnodes != nullptr) {  // finite shadow rays: the 4-ary shadow tree
+            if (STATS) C.v[ST_W_RAYS]++;
+            L.fl |= LF_WIDE;
+            L.cur = S.wroot;
+          }
         }
       }
       chunk_next = min(chunk_next + (uint32_t)n_idle, chunk_end);
@@ -1955,7 +2056,11 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
     if (trav) {
       if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
       const bool wave_finite = __ballot(in_trav && !(L.fl & LF_FINITE)) == 0;
-      if (in_trav) node_step<TRI_ONLY, STATS, CAP, KIND>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C, cyc_leaf);
+      // one primitive of a leaf per step in triangle scenes only, as in the path kernel (mixed-primitive
+      // scenes measured ~10 % slower with it there)
+      if (in_trav)
+        node_step<TRI_ONLY, STATS, CAP, KIND, TRI_ONLY ? 1 : 0, KIND == 2>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t,
+                                                                            wave_finite, C, cyc_leaf);
     }
     if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
       if (KIND == 2) {

@@ -35,11 +35,20 @@ enum StatSlot : int {
   ST_PUSH, ST_PUSH_SPILL,
   // node loop: wave iterations that ran the leaf block, and s_memtime cycles spent in it
   ST_WAVE_LEAF_ITERS, ST_CYC_LEAF,
+  // shadow queries on the 4-ary shadow tree (drt_layout.hpp): queries, inner-node visits, leaf
+  // visits, primitive tests and exact leaf-box checks of in-range hits (the ST_S_* slots then
+  // count only the shadow queries that walked the reference's binary tree)
+  ST_W_RAYS, ST_W_INNER, ST_W_LEAF, ST_W_PRIMS, ST_W_VERIFY,
   ST_COUNT
 };
 
 constexpr int kMaxFrames = 16;     // max_depth <= 15
 constexpr int kMaxBvhDepth = 96;   // traversal stack entries (host rejects deeper trees)
+// A shadow-tree lane keeps its stack in the LDS rows of both the descriptor and the t part (it has
+// no entry distances) and spills past them: 2 * CAP + (kMaxBvhDepth - CAP) >= kMaxBvhDepth + 9
+// entries at every occupancy the kernels use (CAP >= 9).  A 4-ary node pushes at most 3, so the
+// host collapses a tree only when 3 * its depth fits.
+constexpr int kWideMaxStack = kMaxBvhDepth + 8;
 constexpr int kLdsStack = 16;      // traversal stack entries kept in LDS per thread
 constexpr int kBlock = 256;        // path-kernel block size
 #ifndef DRT_PBLOCK
@@ -89,6 +98,11 @@ struct SceneArgs {
   const float4* cell_recs;  // per reference, in cell order: the primitive record, q2.w = its index
   int gmacro_shift, gmacro_dim[3], gmacro_words;
   const uint2* big_leaves;
+  // 4-ary shadow tree (drt_layout.hpp): null = every shadow query walks the reference's binary
+  // tree in its visit order (DRT_FRAME_REFERENCE_ORDER, or a tree the host could not collapse)
+  const float4* wnodes;
+  const float4* wleaf;  // exact reference leaf box per primitive (BVH object order)
+  uint32_t wroot;       // the root's wide record
 };
 
 struct FrameArgs {

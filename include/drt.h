@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DRT_ABI_VERSION 2
+#define DRT_ABI_VERSION 3
 #define DRT_FRAME_SLOTS 4 /* drt_frame_params.slot: 0 .. DRT_FRAME_SLOTS-1 */
 
 typedef enum {
@@ -126,8 +126,14 @@ typedef struct {
 
 /* drt_frame_params.flags: DRT_FRAME_STATS counts rays / node visits / primitive tests;
  * DRT_FRAME_SHARD_LAYOUT makes drt_render_device write the shard-compact tile buffer of
- * drt_shard_layout() even for n_shards == 1 (a one-device drt_group) */
-enum { DRT_FRAME_STATS = 1, DRT_FRAME_SHARD_LAYOUT = 2 };
+ * drt_shard_layout() even for n_shards == 1 (a one-device drt_group);
+ * DRT_FRAME_REFERENCE_ORDER (also a drt_set_trace_flags flag) walks every shadow query
+ * (BVH::Traverse(Ray&), bvh.cpp:316-391) on the reference's binary tree in its visit order, so
+ * that the shadow node / leaf / primitive counts equal the reference's.  Without it, shadow
+ * queries of finite rays walk a 4-ary tree collapsed from the same BVH: the occlusion answer,
+ * hence every frame, is identical (an any-hit query does not depend on the visit order), and
+ * drt_frame_stats counts that work in its wide_* fields. */
+enum { DRT_FRAME_STATS = 1, DRT_FRAME_SHARD_LAYOUT = 2, DRT_FRAME_REFERENCE_ORDER = 4 };
 
 typedef struct {
   uint32_t seed;       /* keyed-RNG seed                                                */
@@ -170,7 +176,12 @@ typedef struct {
    * and taken up again (0 when the hand-over was off for the frame); filled for every frame */
   uint64_t seq_pushed, seq_popped;
   int32_t seq_handover;                   /* the hand-over was on for the frame                  */
-  int32_t reserved[3];
+  int32_t reserved;
+  /* shadow queries that walked the 4-ary shadow tree (not DRT_FRAME_REFERENCE_ORDER): queries,
+   * inner-node visits, leaf visits, primitive tests, exact leaf-box checks of in-range hits.
+   * shadow_inner / shadow_leaf / shadow_prims then count only the queries (non-finite rays)
+   * that walked the reference's binary tree. */
+  uint64_t wide_shadow_rays, wide_inner, wide_leaf, wide_prims, wide_verify;
 } drt_frame_stats;
 
 int drt_create(drt_ctx** out, const drt_options* opt);

@@ -57,6 +57,19 @@ SYNTH_MAT = "mat 1 0.9 0.7 0.5 1 1 1 0.5 30.0827 0 1"
 SYNTH_LIGHTS = ["light quad 4 3 2 1 1 1 4 2 2 3 3 2 16", "light punctual -3 1 5 1 1 1"]
 
 
+def write_synthetic_p3f(path, n_tris, res=(512, 512), spp=64, accel="bvh", seed=1, aperture=0.0, focal=1.0):
+    """synthetic_scene_text written fast for large n (np.savetxt, '%.9g' floats: every float32
+    round-trips through strtof exactly, so the parsed scene is the same).  Returns the path."""
+    tris = np.concatenate([synthetic_triangles(n_tris, seed), FLOOR]).reshape(-1, 3, 3)
+    n = len(tris)
+    lines = header(res=res, spp=spp, accel=accel, aperture=aperture, focal=focal) + SYNTH_LIGHTS + [SYNTH_MAT]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + f"\nmesh {3 * n} {n}\n")
+        np.savetxt(f, tris.reshape(-1, 3), fmt="%.9g")
+        np.savetxt(f, np.arange(1, 3 * n + 1, dtype=np.int64).reshape(n, 3), fmt="%d")
+    return path
+
+
 def synthetic_scene_text(n_tris, res=(512, 512), spp=64, accel="bvh", seed=1, aperture=0.0, focal=1.0):
     """The §8d benchmark scene: triangle soup + floor, one quad and one point light."""
     lines = header(res=res, spp=spp, accel=accel, aperture=aperture, focal=focal)

@@ -64,11 +64,27 @@ def assert_same_work(accel, st, rst):
 
 
 def assert_same_work_frame(renderer, img, rst, seed, **kw):
-    """Re-render a frame with the kernel's stats build: the same frame bit for bit, and the
-    oracle's traversal work (assert_same_work)."""
-    img_s = renderer.render(seed=seed, stats=True, **kw)
+    """Re-render a frame with the kernel's stats build, its shadow queries on the reference's
+    binary tree in the reference's visit order (DRT_FRAME_REFERENCE_ORDER): the same frame bit for
+    bit as `img` (rendered with the default 4-ary shadow tree), and the oracle's traversal work
+    (assert_same_work)."""
+    img_s = renderer.render(seed=seed, stats=True, reference_order=True, **kw)
     np.testing.assert_array_equal(bits(img_s), bits(img))
     assert_same_work(renderer.scene.info().accel, renderer.stats(), rst)
+
+
+def assert_shadow_tree_work(accel, st, rst):
+    """A default frame: closest-hit work equal to the oracle's, every shadow query counted, and
+    the shadow queries of finite rays on the 4-ary shadow tree (DRT_FRAME_REFERENCE_ORDER off)."""
+    if accel == 0:
+        return
+    assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
+    for k in ("closest_leaf", "closest_prims") + (("closest_inner",) if accel == 2 else ()):
+        assert st[k] == rst[k], (k, st[k], rst[k])
+    if accel != 2:
+        assert st["wide_shadow_rays"] == 0
+    elif st["shadow_rays"]:
+        assert st["wide_shadow_rays"] > 0
 
 
 GOLD_CASES = ["tiny", "mixed", "tris2k"]
@@ -88,7 +104,14 @@ def test_bvh_traverse_matches_reference_golden(drt, renderer, tmp_path, case):
     np.testing.assert_array_equal(obj, g["bvh_obj"])
     np.testing.assert_array_equal(bits(t), bits(g["bvh_t"]))
     np.testing.assert_array_equal(bits(n), bits(g["bvh_n"]))
-    np.testing.assert_array_equal(renderer.trace_shadow(g["shadow_rays"]), g["bvh_occ"])
+    np.testing.assert_array_equal(renderer.trace_shadow(g["shadow_rays"]), g["bvh_occ"])  # 4-ary shadow tree
+    renderer.set_trace_stats(True, reference_order=True)
+    try:
+        np.testing.assert_array_equal(renderer.trace_shadow(g["shadow_rays"]), g["bvh_occ"])  # the reference's tree
+        st = renderer.trace_stats()
+        assert st["wide_shadow_rays"] == 0 and st["shadow_rays"] == len(g["shadow_rays"])
+    finally:
+        renderer.set_trace_stats(False)
 
 
 @pytest.mark.parametrize("case", ["mixed", "tris2k"])
@@ -184,9 +207,12 @@ def test_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
     st = renderer.stats()
     ref, rst = b.render(seed=seed, **kw)
     compare_images(img, ref)
-    # identical branching => identical traversal work
-    assert_same_work(a.info().accel, st, rst)
+    assert_shadow_tree_work(a.info().accel, st, rst)
     assert st["samples"] == rst["samples"]
+    # the reference's shadow visit order: the same frame bit for bit, identical traversal work
+    img_r = renderer.render(seed=seed, stats=True, reference_order=True, **kw)
+    np.testing.assert_array_equal(bits(img_r), bits(img))
+    assert_same_work(a.info().accel, renderer.stats(), rst)
 
 
 @pytest.mark.parametrize("accel,aperture,roughness", [("bvh", 0.0, 0.0), ("bvh", 8.0, 0.2), ("grid", 0.0, 0.0),
@@ -199,12 +225,13 @@ def test_progressive_matches_oracle(drt, oracle_mod, renderer, tmp_path, accel, 
     acc_g = np.zeros((16, 24, 3), np.float32)
     acc_o = np.zeros((16, 24, 3), np.float32)
     for n in (1, 2, 3):
-        renderer.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_g, stats=True)
+        renderer.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_g, stats=True,
+                        reference_order=n % 2 == 1)
         st = renderer.stats()
         _, rst = b.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_o)
         compare_images(acc_g, acc_o)
         assert st["samples"] == rst["samples"] == 24 * 16
-        assert_same_work(a.info().accel, st, rst)
+        (assert_same_work if n % 2 == 1 else assert_shadow_tree_work)(a.info().accel, st, rst)
     before = acc_g.copy()
     renderer.render(seed=9, progressive_frame=10000, accum=acc_g)  # MAX_SAMPLES: untouched
     np.testing.assert_array_equal(acc_g, before)
@@ -240,6 +267,25 @@ def test_camera_orbit_without_reupload(drt, oracle_mod, renderer, tmp_path, acce
     ref, _ = b.render(seed=9)
     compare_images(renderer.render(seed=9), ref)
     fresh.close()
+
+
+def test_set_camera_refuses_a_new_resolution(drt, renderer, tmp_path):
+    """Camera::SetEye keeps the resolution (camera.h:63-72) and the caller's frame buffers are sized
+    by the resident one: drt_set_camera (and drt_group_set_camera, validated on every device before
+    any changes) refuses a camera of another resolution and leaves the resident camera in place."""
+    a = drt.Scene.load_p3f(sg.write(tmp_path, "a.p3f", sg.mixed_scene_text(res=(32, 24), spp=1, n_tris=40)))
+    big = drt.Scene.load_p3f(sg.write(tmp_path, "b.p3f", sg.mixed_scene_text(res=(64, 48), spp=1, n_tris=40)))
+    renderer.upload(a)
+    before = renderer.render(seed=3)
+    with pytest.raises(RuntimeError, match="DRT_E_INVALID"):
+        renderer.set_camera(big)
+    np.testing.assert_array_equal(bits(renderer.render(seed=3)), bits(before))
+    g = drt.RendererGroup([0])
+    g.upload(a)
+    with pytest.raises(RuntimeError, match="DRT_E_INVALID"):
+        g.set_camera(big)
+    np.testing.assert_array_equal(bits(g.render(seed=3)), bits(before))
+    g.close()
 
 
 def test_set_camera_host_overhead_at_1M_triangles(drt, renderer):
@@ -608,7 +654,8 @@ def test_grid_stepper_caps_do_not_change_the_frame(drt, renderer, monkeypatch, w
     img = renderer.render(seed=11, stats=True)
     st = renderer.stats()
     np.testing.assert_array_equal(bits(img), bits(ref))
-    for k in ("closest_rays", "shadow_rays", "closest_leaf", "shadow_leaf", "closest_prims", "shadow_prims", "samples"):
+    for k in ("closest_rays", "shadow_rays", "closest_leaf", "shadow_leaf", "closest_prims", "shadow_prims", "samples",
+            "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify"):
         assert st[k] == rst[k], k
 
 
@@ -624,7 +671,8 @@ def test_node_record_layout_does_not_change_the_frame(drt, renderer, monkeypatch
     bench.populate(s, bench.synthetic_triangles(1_000_000), 96, 4)
     s.build()
     keys = ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
-            "closest_prims", "shadow_prims", "samples")
+            "closest_prims", "shadow_prims", "samples",
+            "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify")
     out = {}
     for lay in ("1", layout):
         monkeypatch.setenv("DRT_NODE_LAYOUT", lay)
@@ -669,7 +717,8 @@ def test_seq_tail_handover_does_not_change_the_frame(drt, renderer, tmp_path, mo
         st = renderer.stats()
         np.testing.assert_array_equal(bits(img), bits(ref), err_msg=f"backlog {backlog}")
         for k in ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
-                  "closest_prims", "shadow_prims", "samples"):
+                  "closest_prims", "shadow_prims", "samples",
+            "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify"):
             assert st[k] == rst[k], (backlog, k)
         # the hand-over happened: pixels were pushed, and every push was popped by a kept wave
         assert st["seq_handover"] == 1
@@ -747,7 +796,8 @@ def test_two_pass_in_order_frame_equals_one_pass(drt, renderer, tmp_path, monkey
     rst = renderer.stats()
     np.testing.assert_array_equal(bits(img), bits(ref))
     for k in ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
-              "closest_prims", "shadow_prims", "samples"):
+              "closest_prims", "shadow_prims", "samples",
+            "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify"):
         assert st[k] == rst[k], k
     monkeypatch.delenv("DRT_SEQ_TWO_PASS")
     glass = sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", n_tris=40, aperture=8.0, focal=1.5)
