@@ -94,6 +94,7 @@ struct drt_ctx {
   int gdim[3] = {0, 0, 0};
   float gmin[3] = {0}, gmax[3] = {0};
   DevBuf d_cell_start, d_cell_objs, d_macro, d_cell_recs;
+  DevBuf d_gprims, d_cell_pos;  // indexed Grid layout (experiment): Morton-ordered records, per-reference positions
   int gmacro_shift = 0, gmacro_dim[3] = {0, 0, 0}, gmacro_words = 0;
   // frame scratch
   DevBuf d_frame, d_rays, d_out, d_counter;
@@ -674,6 +675,47 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
     DRT_HIP(c, hipMemset(c->d_cell_recs.p, 0, sizeof(PrimRecord) * recs.size() + kPrimPadBytes));
     DRT_HIP(c, hipMemcpy(c->d_cell_recs.p, recs.data(), sizeof(PrimRecord) * recs.size(), hipMemcpyHostToDevice));
   }
+  // Indexed layout (experiment, drt_kernels.hip DRT_GRID_INDEXED): every object's record once, in the
+  // order a Morton walk of the non-empty cells first meets it (q2.w = the scene-order index), and per
+  // reference its position there — so that objects of neighbouring cells share lines
+  {
+    auto part = [](uint32_t v) {  // 10 bits -> every third bit
+      v &= 0x3ffu;
+      v = (v | (v << 16)) & 0x030000FFu;
+      v = (v | (v << 8)) & 0x0300F00Fu;
+      v = (v | (v << 4)) & 0x030C30C3u;
+      v = (v | (v << 2)) & 0x09249249u;
+      return v;
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> cells;  // (Morton code, cell)
+    for (int z = 0; z < dims[2]; z++)
+      for (int y = 0; y < dims[1]; y++)
+        for (int x = 0; x < dims[0]; x++) {
+          const size_t ci = (size_t)x + (size_t)dims[0] * y + (size_t)dims[0] * dims[1] * z;
+          if (s32[ci + 1] != s32[ci])
+            cells.push_back({part((uint32_t)x) | (part((uint32_t)y) << 1) | (part((uint32_t)z) << 2), (uint32_t)ci});
+        }
+    std::sort(cells.begin(), cells.end());
+    std::vector<uint32_t> rank((size_t)c->n_prims, UINT32_MAX);
+    uint32_t next = 0;
+    for (auto& mc : cells)
+      for (uint32_t k = s32[mc.second]; k < s32[mc.second + 1]; k++)
+        if (rank[o32[k]] == UINT32_MAX) rank[o32[k]] = next++;
+    for (auto& r : rank)
+      if (r == UINT32_MAX) r = next++;
+    std::vector<PrimRecord> g((size_t)std::max(1, c->n_prims));
+    for (int i = 0; i < c->n_prims; i++) {
+      g[rank[i]] = c->prims_scene[i];
+      memcpy(&g[rank[i]].q[11], &i, 4);
+    }
+    std::vector<uint32_t> pos((size_t)n_refs + 2, 0u);  // + 2: the stepper reads pairs
+    for (int64_t i = 0; i < n_refs; i++) pos[i] = rank[o32[i]];
+    DRT_HIP(c, c->d_gprims.ensure(sizeof(PrimRecord) * g.size() + kPrimPadBytes));
+    DRT_HIP(c, hipMemset(c->d_gprims.p, 0, sizeof(PrimRecord) * g.size() + kPrimPadBytes));
+    DRT_HIP(c, hipMemcpy(c->d_gprims.p, g.data(), sizeof(PrimRecord) * g.size(), hipMemcpyHostToDevice));
+    DRT_HIP(c, c->d_cell_pos.ensure(4 * pos.size()));
+    DRT_HIP(c, hipMemcpy(c->d_cell_pos.p, pos.data(), 4 * pos.size(), hipMemcpyHostToDevice));
+  }
   // grid references index scene-order primitive records
   DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
                        hipMemcpyHostToDevice));
@@ -746,6 +788,8 @@ static int scene_args(drt_ctx* c, int accel, SceneArgs& S, bool reference_order)
     S.cell_start = c->d_cell_start.as<uint32_t>();
     S.gmacro = c->d_macro.as<uint32_t>();
     S.cell_recs = c->d_cell_recs.as<float4>();
+    S.gprims = c->d_gprims.as<float4>();
+    S.cell_pos = c->d_cell_pos.as<uint32_t>();
     S.gmacro_shift = c->gmacro_shift;
     memcpy(S.gmacro_dim, c->gmacro_dim, sizeof(S.gmacro_dim));
     S.gmacro_words = c->gmacro_words;

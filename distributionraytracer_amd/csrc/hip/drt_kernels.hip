@@ -968,8 +968,21 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
 #ifdef DRT_GRID_DIAG
     if (STATS && wave_leader()) C.v[ST_WAVE_LEAF_ITERS]++;  // pair-loop wave iterations
 #endif
-    const float4* r = S.cell_recs + 3 * (size_t)q;
     const bool two = q + 1 < e;
+#ifdef DRT_GRID_INDEXED
+    uint2 ix;  // the pair's record positions (one 8-B load, 4-B aligned)
+    __builtin_memcpy(&ix, S.cell_pos + q, sizeof(ix));
+    const float4* r = S.gprims + 3 * (size_t)ix.x;
+    const float4* r2 = S.gprims + 3 * (size_t)ix.y;
+    const float4 a0 = r[0], a1 = r[1], a2 = r[2];
+    float4 c0, c1, c2;
+    if (two) {
+      c0 = r2[0];
+      c1 = r2[1];
+      c2 = r2[2];
+    }
+#else
+    const float4* r = S.cell_recs + 3 * (size_t)q;
     const float4 a0 = r[0], a1 = r[1], a2 = r[2];
     float4 c0, c1, c2;
     if (two) {
@@ -977,6 +990,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
       c1 = r[4];
       c2 = r[5];
     }
+#endif
     test(a0, a1, a2);
     if (!done && two) test(c0, c1, c2);
     if (done) {

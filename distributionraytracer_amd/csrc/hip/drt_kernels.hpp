@@ -96,6 +96,8 @@ struct SceneArgs {
   // cell of that macro-cell holds an object
   const uint32_t* gmacro;
   const float4* cell_recs;  // per reference, in cell order: the primitive record, q2.w = its index
+  const float4* gprims;     // (experiment DRT_GRID_INDEXED) each record once, Morton cell order, q2.w = index
+  const uint32_t* cell_pos; // (experiment DRT_GRID_INDEXED) per reference: its record in gprims
   int gmacro_shift, gmacro_dim[3], gmacro_words;
   const uint2* big_leaves;
   // 4-ary shadow tree (drt_layout.hpp): null = every shadow query walks the reference's binary

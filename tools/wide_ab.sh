@@ -32,6 +32,12 @@ for rep in 1 2; do
   ab C3 DRT_WIDE_SHADOW=1 --tris 100000 --light-spp 4 || exit $?
   ab C3 DRT_WIDE_SHADOW=0 --tris 100000 --light-spp 4 || exit $?
 done
+if [ "${GRID:-0}" = "1" ]; then  # Grid layout experiment: inline records vs the Morton-indexed variant
+  for rep in 1 2; do
+    ab grid_inline DRT_WIDE_SHADOW=1 --accel grid || exit $?
+    ab grid_indexed DRT_LIBRARY=distributionraytracer_amd/csrc/build/alt/libdrt_gidx.so --accel grid || exit $?
+  done
+fi
 if [ "${C4:-1}" = "1" ]; then
   ab C4 DRT_WIDE_SHADOW=1 --res 1024 --aperture 8 --focal 1 --max-depth 8 --roughness 0.1 --steps 3 || exit $?
   ab C4 DRT_WIDE_SHADOW=0 --res 1024 --aperture 8 --focal 1 --max-depth 8 --roughness 0.1 --steps 3 || exit $?
