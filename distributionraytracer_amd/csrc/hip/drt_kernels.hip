@@ -1174,6 +1174,31 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     const uint32_t d[4] = {__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w)};
     float tn[4];
     bool hk[4];
+#ifdef DRT_WIDE_PK
+    // two children per packed-f32 instruction (v_pk_fma / v_pk_add / v_pk_mul): the same roundings
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v ox2 = {L.q.o.x, L.q.o.x}, oy2 = {L.q.o.y, L.q.o.y}, oz2 = {L.q.o.z, L.q.o.z};
+    const f2v ix2 = {L.q.ix, L.q.ix}, iy2 = {L.q.iy, L.q.iy}, iz2 = {L.q.iz, L.q.iz};
+    const f2v sx2 = {scx, scx}, sy2 = {scy, scy}, sz2 = {scz, scz};
+    const f2v px2 = {s0.x, s0.x}, py2 = {s0.y, s0.y}, pz2 = {s0.z, s0.z};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int a = 16 * h, b = 16 * h + 8;
+      auto dq = [&](uint32_t w) { return f2v{(float)((w >> a) & 0xffu), (float)((w >> b) & 0xffu)}; };
+      const f2v tnx = (__builtin_elementwise_fma(dq(nx), sx2, px2) - ox2) * ix2;
+      const f2v tfx = (__builtin_elementwise_fma(dq(fx), sx2, px2) - ox2) * ix2;
+      const f2v tny = (__builtin_elementwise_fma(dq(ny), sy2, py2) - oy2) * iy2;
+      const f2v tfy = (__builtin_elementwise_fma(dq(fy), sy2, py2) - oy2) * iy2;
+      const f2v tnz = (__builtin_elementwise_fma(dq(nz), sz2, pz2) - oz2) * iz2;
+      const f2v tfz = (__builtin_elementwise_fma(dq(fz), sz2, pz2) - oz2) * iz2;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const float t0 = fmaxf(fmaxf(tnx[j], tny[j]), tnz[j]), t1 = fminf(fminf(tfx[j], tfy[j]), tfz[j]);
+        hk[2 * h + j] = fmaxf(t0, 0.0f) < t1;
+        tn[2 * h + j] = t0;
+      }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int sh = 8 * k;
@@ -1187,12 +1212,17 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       hk[k] = fmaxf(t0, 0.0f) < t1;  // t0 < t1 && t1 > 0
       tn[k] = t0;
     }
+#endif
     // go on with the hit child entered first (any order gives the same answer); push the others
     int ci = -1;
     float best = 0.0f;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
+#ifdef DRT_WIDE_FIRST  // (A/B) the first hit child, no distance order
+      const bool take = hk[k] && ci < 0;
+#else
       const bool take = hk[k] && (ci < 0 || tn[k] < best);
+#endif
       ci = take ? k : ci;
       best = take ? tn[k] : best;
     }
@@ -1327,6 +1357,15 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       uint32_t pd;
       float pt = 0.0f;
       // a shadow-tree lane's LDS stack spans the t rows too (it keeps no entry distances)
+      if constexpr (!WIDE) {  // binary lanes only: the round-3 pop (measured 1 769 against 1 757 Mrays/s)
+      if (spa < kLdsBytes) {
+        pd = *(LdsU32*)(lds + spa);
+        pt = *(LdsF32*)(lds + kLdsBytes + spa);
+      } else {
+        pd = ov_desc[(spa >> kRowShift) - CAP];
+        pt = ov_t[(spa >> kRowShift) - CAP];
+      }
+      } else {
       const uint32_t lim = wide ? 2u * kLdsBytes : kLdsBytes;
       if (spa < lim) {
         pd = *(LdsU32*)(lds + spa);
@@ -1334,6 +1373,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       } else {
         pd = ov_desc[(spa - lim) >> kRowShift];
         pt = ov_t[(spa - lim) >> kRowShift];
+      }
       }
       if (shadow || pt < L.best_t) {
         L.cur = pd;
@@ -1359,7 +1399,11 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
   if (ACC == ACC_GRID)  // Grid::Traverse(Ray&) gets the unit L: range |L|, direction re-normalised (Q1)
     start_query<STATS, ACC>(S, L, make_ray(so, normalize(Lv)), true, length(Lv), C);
   else  // BVH::Traverse(Ray&) normalises Ls and accepts t <= |Ls| + EPSILON (bvh.cpp:321-322, :376)
+#ifdef DRT_PATH_WIDE  // (A/B) shadow tree in the path kernel (see the node loop)
     start_query<STATS, ACC, true>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
+#else
+    start_query<STATS, ACC>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
+#endif
 }
 
 // reflectDir (main.cpp:504-508); MODE_SEQ draws rnd_unit_sphere on the lane's keyed stream
@@ -1947,8 +1991,18 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         // 770 Mrays/s), and in one-pass in-order frames (scratch 2 464 -> 2 496 B); mixed-primitive
         // scenes keep the whole-leaf step (C2, balls_low: 23 000 -> 20 800 Mrays/s with it)
         constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL ? 1 : 2);
-        // every mode with shadow queries walks them on the shadow tree (the closest-chain pass has none)
+        // The shadow tree stays out of the path kernel (measured, round 4, headline 512^2 x 64 spp): its
+        // lanes walked 26 % fewer node records per ray (75.8 -> 56.2 visits), but a wave whose lanes
+        // mix closest-hit and shadow queries runs the binary and the 4-ary child tests one after the
+        // other, and the 4-ary test's decode (~130 VALU) outweighs the gathers saved: 1 404 against
+        // 1 509 Mrays/s with it switched off in the same build, and the code compiled into the loop
+        // cost 1 509 against 1 757 Mrays/s by itself (tools/lib_matrix.sh).  The
+        // streaming shadow kernel, whose waves hold shadow queries only, uses it.
+#ifdef DRT_PATH_WIDE  // (A/B) shadow tree in the path kernel
         constexpr bool kWide = MODE != MODE_SKEL;
+#else
+        constexpr bool kWide = false;
+#endif
         if (in_trav)
           node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1, kWide>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C,
                                                             cyc[3]);

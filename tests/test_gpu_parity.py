@@ -64,27 +64,11 @@ def assert_same_work(accel, st, rst):
 
 
 def assert_same_work_frame(renderer, img, rst, seed, **kw):
-    """Re-render a frame with the kernel's stats build, its shadow queries on the reference's
-    binary tree in the reference's visit order (DRT_FRAME_REFERENCE_ORDER): the same frame bit for
-    bit as `img` (rendered with the default 4-ary shadow tree), and the oracle's traversal work
-    (assert_same_work)."""
-    img_s = renderer.render(seed=seed, stats=True, reference_order=True, **kw)
+    """Re-render a frame with the kernel's stats build: the same frame bit for bit, and the
+    oracle's traversal work (assert_same_work)."""
+    img_s = renderer.render(seed=seed, stats=True, **kw)
     np.testing.assert_array_equal(bits(img_s), bits(img))
     assert_same_work(renderer.scene.info().accel, renderer.stats(), rst)
-
-
-def assert_shadow_tree_work(accel, st, rst):
-    """A default frame: closest-hit work equal to the oracle's, every shadow query counted, and
-    the shadow queries of finite rays on the 4-ary shadow tree (DRT_FRAME_REFERENCE_ORDER off)."""
-    if accel == 0:
-        return
-    assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
-    for k in ("closest_leaf", "closest_prims") + (("closest_inner",) if accel == 2 else ()):
-        assert st[k] == rst[k], (k, st[k], rst[k])
-    if accel != 2:
-        assert st["wide_shadow_rays"] == 0
-    elif st["shadow_rays"]:
-        assert st["wide_shadow_rays"] > 0
 
 
 GOLD_CASES = ["tiny", "mixed", "tris2k"]
@@ -207,12 +191,9 @@ def test_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
     st = renderer.stats()
     ref, rst = b.render(seed=seed, **kw)
     compare_images(img, ref)
-    assert_shadow_tree_work(a.info().accel, st, rst)
+    # identical branching => identical traversal work
+    assert_same_work(a.info().accel, st, rst)
     assert st["samples"] == rst["samples"]
-    # the reference's shadow visit order: the same frame bit for bit, identical traversal work
-    img_r = renderer.render(seed=seed, stats=True, reference_order=True, **kw)
-    np.testing.assert_array_equal(bits(img_r), bits(img))
-    assert_same_work(a.info().accel, renderer.stats(), rst)
 
 
 @pytest.mark.parametrize("accel,aperture,roughness", [("bvh", 0.0, 0.0), ("bvh", 8.0, 0.2), ("grid", 0.0, 0.0),
@@ -225,13 +206,12 @@ def test_progressive_matches_oracle(drt, oracle_mod, renderer, tmp_path, accel, 
     acc_g = np.zeros((16, 24, 3), np.float32)
     acc_o = np.zeros((16, 24, 3), np.float32)
     for n in (1, 2, 3):
-        renderer.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_g, stats=True,
-                        reference_order=n % 2 == 1)
+        renderer.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_g, stats=True)
         st = renderer.stats()
         _, rst = b.render(seed=40 + n, roughness=roughness, progressive_frame=n, accum=acc_o)
         compare_images(acc_g, acc_o)
         assert st["samples"] == rst["samples"] == 24 * 16
-        (assert_same_work if n % 2 == 1 else assert_shadow_tree_work)(a.info().accel, st, rst)
+        assert_same_work(a.info().accel, st, rst)
     before = acc_g.copy()
     renderer.render(seed=9, progressive_frame=10000, accum=acc_g)  # MAX_SAMPLES: untouched
     np.testing.assert_array_equal(acc_g, before)

@@ -104,8 +104,9 @@ def test_shadow_tree_equals_reference_order_on_1e7_frame_shadow_rays(drt, render
     wide, ref, st_w, st_r = trace_shadow_both(renderer, rays)
     np.testing.assert_array_equal(wide, ref)
     assert 0.05 < wide.mean() < 0.95  # both answers occur
-    assert st_w["wide_shadow_rays"] == len(rays) and st_r["wide_shadow_rays"] == 0
-    assert st_w["shadow_inner"] == 0 and st_r["shadow_inner"] > 0
+    # the few rays with a zero direction component keep the reference's tree (its slab NaN rules)
+    assert len(rays) - 100 < st_w["wide_shadow_rays"] <= len(rays) and st_r["wide_shadow_rays"] == 0
+    assert st_w["shadow_inner"] < 0.001 * st_r["shadow_inner"]
     # the point of the tree: fewer node records per query
     assert st_w["wide_inner"] < 0.75 * st_r["shadow_inner"], (st_w["wide_inner"], st_r["shadow_inner"])
     print(f"\n{len(rays)} shadow rays, occluded {wide.mean():.3f}: per query wide inner {st_w['wide_inner'] / len(rays):.2f} "
@@ -137,21 +138,18 @@ def test_shadow_tree_matches_oracle_on_mixed_primitives(drt, oracle_mod, rendere
     assert st_w["wide_shadow_rays"] < len(rays)  # the non-finite rays keep the reference's tree
 
 
-def test_shadow_tree_off_and_on_render_the_same_frames(drt, renderer, monkeypatch):
-    """DRT_WIDE_SHADOW=0 uploads no shadow tree: frames equal the default frames bit for bit on the
-    100k-triangle C3 workload (4 light samples, AA) and a glossy depth-6 frame (two passes)."""
+def test_frames_render_every_shadow_query_on_the_reference_tree(drt, renderer):
+    """The path kernel walks shadow queries on the reference's tree (the shadow tree measured slower
+    there): frame stats count no shadow-tree work, with or without the frame flag."""
     import bench
 
     s = drt.Scene()
-    bench.populate(s, bench.synthetic_triangles(100_000), 96, 8)
+    bench.populate(s, bench.synthetic_triangles(20_000), 48, 4)
     s.build()
-    out = {}
-    for wide in ("1", "0"):
-        monkeypatch.setenv("DRT_WIDE_SHADOW", wide)
-        renderer.upload(s)
-        out[wide] = [renderer.render(seed=4, stats=True, **kw).view(np.uint32) for kw in
-                     ({"light_spp": 4}, {"roughness": 0.1, "max_depth": 6})]
-        st = renderer.stats()
-        assert (st["wide_shadow_rays"] > 0) == (wide == "1")
-    for a, b in zip(out["1"], out["0"]):
-        np.testing.assert_array_equal(a, b)
+    renderer.upload(s)
+    a = renderer.render(seed=4, stats=True)
+    st = renderer.stats()
+    b = renderer.render(seed=4, stats=True, reference_order=True)
+    assert st["wide_shadow_rays"] == 0 and st["shadow_rays"] > 0
+    assert st == {**renderer.stats(), "kernel_ms": st["kernel_ms"], "render_ms": st["render_ms"]}
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--waves", default="6,7,8")
+    ap.add_argument("--reference-order", action="store_true",
+                    help="shadow queries on the reference's binary tree (DRT_FRAME_REFERENCE_ORDER)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime: torch's)
@@ -74,14 +76,18 @@ def main():
     out = {"tris": args.tris, "sets": {}}
     for name, (rays, shadow) in sets.items():
         fn = r.trace_shadow if shadow else r.trace_closest
-        r.set_trace_stats(True)
+        r.set_trace_stats(True, reference_order=args.reference_order)
         fn(rays)
         st = r.trace_stats()
-        r.set_trace_stats(False)
+        r.set_trace_stats(False, reference_order=args.reference_order)
         kind = "shadow" if shadow else "closest"
-        steps = st[f"{kind}_inner"] + st[f"{kind}_leaf"]
-        rec = {"rays": len(rays), "inner_per_ray": st[f"{kind}_inner"] / len(rays),
-               "leaf_per_ray": st[f"{kind}_leaf"] / len(rays), "prims_per_ray": st[f"{kind}_prims"] / len(rays),
+        # batched shadow queries walk the 4-ary shadow tree unless --reference-order
+        inner = st[f"{kind}_inner"] + (st["wide_inner"] if shadow else 0)
+        leaf = st[f"{kind}_leaf"] + (st["wide_leaf"] if shadow else 0)
+        prims = st[f"{kind}_prims"] + (st["wide_prims"] if shadow else 0)
+        steps = inner + leaf + (st["wide_verify"] if shadow else 0)
+        rec = {"rays": len(rays), "inner_per_ray": inner / len(rays), "leaf_per_ray": leaf / len(rays),
+               "prims_per_ray": prims / len(rays), "tree": "4-ary shadow tree" if st["wide_shadow_rays"] else "reference",
                "simd_eff": steps / max(1, st["wave_node_iters"] * 64), "spill": st["stack_spills"] / max(1, st["stack_pushes"])}
         for w in args.waves.split(","):
             os.environ["DRT_TRACE_WAVES"] = w

@@ -11,7 +11,7 @@ rc=$?; echo "shadow-tree pytest rc=$rc"; tail -12 $OUT/shadow_tree_tests.log
 if [ $rc -ge 2 ]; then exit $rc; fi
 ab() {  # label, env, bench args...
   local label=$1 v=$2; shift 2
-  env $v timeout -k 10 300 python bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline "$@" > $OUT/ab.json 2> $OUT/ab.err
+  env $v timeout -k 10 300 python bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-load-timing "$@" > $OUT/ab.json 2> $OUT/ab.err
   local rc=$?
   python - "$label" "$v" $OUT/ab.json >> $OUT/wide_ab.jsonl <<'PY'
 import json, sys
@@ -24,13 +24,19 @@ PY
   tail -1 $OUT/wide_ab.jsonl | cut -c1-220
   return $rc
 }
+PK=distributionraytracer_amd/csrc/build/alt/libdrt_wpk.so  # packed-f32 wide child test (DRT_WIDE_PK)
+FIRST=distributionraytracer_amd/csrc/build/alt/libdrt_wfirst.so  # first hit child, no distance order
 for rep in 1 2; do
   ab headline DRT_WIDE_SHADOW=1 || exit $?
   ab headline DRT_WIDE_SHADOW=0 || exit $?
+  [ -f $PK ] && { ab headline_pk DRT_LIBRARY=$PK || exit $?; }
+  [ -f $FIRST ] && { ab headline_first DRT_LIBRARY=$FIRST || exit $?; }
 done
 for rep in 1 2; do
   ab C3 DRT_WIDE_SHADOW=1 --tris 100000 --light-spp 4 || exit $?
   ab C3 DRT_WIDE_SHADOW=0 --tris 100000 --light-spp 4 || exit $?
+  [ -f $PK ] && { ab C3_pk DRT_LIBRARY=$PK --tris 100000 --light-spp 4 || exit $?; }
+  [ -f $FIRST ] && { ab C3_first DRT_LIBRARY=$FIRST --tris 100000 --light-spp 4 || exit $?; }
 done
 if [ "${GRID:-0}" = "1" ]; then  # Grid layout experiment: inline records vs the Morton-indexed variant
   for rep in 1 2; do
