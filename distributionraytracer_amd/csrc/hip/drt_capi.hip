@@ -804,6 +804,7 @@ struct Plan {
   int tiles_y, n_tiles;
   bool persistent;      // path_persistent (BVH) instead of path_kernel
   bool two_pass;        // in-order frame as MODE_SKEL + MODE_REPLAY (no refraction in the scene)
+  bool aa_chain;        // ... or an AA frame as MODE_CHAIN + MODE_REPLAY (BVH, shadow tree uploaded)
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -886,6 +887,20 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
     for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
     P.two_pass = !refr;
   }
+  // AA frames in two passes (round 4): the samples' closest-hit chains (MODE_CHAIN, one lane per
+  // sample), then every sample's shading with its closest hits read back (MODE_REPLAY), whose waves
+  // then hold shadow queries only and walk them on the 4-ary shadow tree.  In one pass the lanes of a
+  // wave mix both query kinds and the shadow tree measured slower.  Same conditions
+  // as above (no refraction, the record fits), a BVH with its shadow tree, and not a reference-order
+  // frame (DRT_FRAME_REFERENCE_ORDER keeps the one-pass frame); DRT_AA_TWO_PASS=0 keeps one pass.
+  P.aa_chain = false;
+  if (P.persistent && F.mode == MODE_AA && c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide &&
+      !(p->flags & DRT_FRAME_REFERENCE_ORDER) && env_int("DRT_AA_TWO_PASS", 1) != 0 &&
+      P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
+    bool refr = false;
+    for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
+    P.two_pass = P.aa_chain = !refr;
+  }
   ReduceArgs& R = P.R;
   R.nsub = slots;
   R.scale = scale;
@@ -929,12 +944,12 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // Two-pass in-order frame: its closest-hit record is allocated first; a frame whose record does not
   // fit in device memory runs as the one-pass MODE_SEQ frame, which renders the same pixels.
   if (P.F.n_items && P.two_pass) {
-    if (c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess ||
+    if ((!P.aa_chain && c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess) ||
         c->d_skel_hits_s[slot].ensure(sizeof(uint2) * P.n_slots * (uint64_t)(P.F.max_depth + 1)) != hipSuccess) {
       (void)hipGetLastError();
       c->d_skel_rk_s[slot].release();
       c->d_skel_hits_s[slot].release();
-      P.two_pass = false;
+      P.two_pass = P.aa_chain = false;
     }
   }
   // MODE_SEQ tail hand-over (DRT_SEQ_DONATE: 0 off, 1 on, default auto).  It frees whole blocks
@@ -1027,10 +1042,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   if (P.F.n_items && P.two_pass) {
     DevBuf& d_rk = c->d_skel_rk_s[slot];  // allocated above
     DevBuf& d_hits = c->d_skel_hits_s[slot];
-    FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order
-    F1.mode = MODE_SKEL;
-    F1.skel_rk = d_rk.as<uint32_t>();
+    FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order (AA: any order)
+    F1.mode = P.aa_chain ? MODE_CHAIN : MODE_SKEL;
+    F1.skel_rk = P.aa_chain ? nullptr : d_rk.as<uint32_t>();
     F1.skel_hits = d_hits.as<uint2>();
+    F1.aa_chain = P.aa_chain ? 1 : 0;
     F1.seq_cont = nullptr;
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());

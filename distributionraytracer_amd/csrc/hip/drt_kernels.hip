@@ -783,7 +783,10 @@ struct Lane {
   uint32_t smp, rk, pmix;
   // ACC_GRID only (dead otherwise): the 3D-DDA of Grid::Traverse in double (grid.cpp:200-245);
   // the cell is packed in `cur` (ix | iy << 10 | iz << 20)
-  double gtx, gty, gtz, gdx, gdy, gdz;
+  // t_next per axis in double; dt per axis is a float widened to double (grid.cpp: dtx =
+  // (txmax - txmin) / nx in float), so it is kept as the float (3 VGPRs instead of 6)
+  double gtx, gty, gtz;
+  float gdx, gdy, gdz;
 };
 // (Measured alternative, kept out: the shading state in a private per-activation frame array
 // instead of registers — the extra scratch stores sit in vmcnt ahead of the next node fetch,
@@ -844,14 +847,14 @@ __device__ __forceinline__ bool grid_init(const SceneArgs& S, Lane& L) {
     iy = dclampi((p.y - y0) * ny / (y1 - y0), ny - 1);
     iz = dclampi((p.z - z0) * nz / (z1 - z0), nz - 1);
   }
-  L.gdx = (double)((txmax - txmin) / (float)nx);
-  L.gdy = (double)((tymax - tymin) / (float)ny);
-  L.gdz = (double)((tzmax - tzmin) / (float)nz);
-  L.gtx = (dx > 0.0f) ? (double)txmin + (ix + 1) * L.gdx : (double)txmin + (nx - ix) * L.gdx;
+  L.gdx = (txmax - txmin) / (float)nx;
+  L.gdy = (tymax - tymin) / (float)ny;
+  L.gdz = (tzmax - tzmin) / (float)nz;
+  L.gtx = (dx > 0.0f) ? (double)txmin + (ix + 1) * (double)L.gdx : (double)txmin + (nx - ix) * (double)L.gdx;
   if (dx == 0.0f) L.gtx = 3.4028234663852886e38;
-  L.gty = (dy > 0.0f) ? (double)tymin + (iy + 1) * L.gdy : (double)tymin + (ny - iy) * L.gdy;
+  L.gty = (dy > 0.0f) ? (double)tymin + (iy + 1) * (double)L.gdy : (double)tymin + (ny - iy) * (double)L.gdy;
   if (dy == 0.0f) L.gty = 3.4028234663852886e38;
-  L.gtz = (dz > 0.0f) ? (double)tzmin + (iz + 1) * L.gdz : (double)tzmin + (nz - iz) * L.gdz;
+  L.gtz = (dz > 0.0f) ? (double)tzmin + (iz + 1) * (double)L.gdz : (double)tzmin + (nz - iz) * (double)L.gdz;
   if (dz == 0.0f) L.gtz = 3.4028234663852886e38;
   L.cur = (uint32_t)ix | ((uint32_t)iy << 10) | ((uint32_t)iz << 20);
   return true;
@@ -1004,7 +1007,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   const int ex = dx > 0.0f ? nx : -1, ey = dy > 0.0f ? ny : -1, ez = dz > 0.0f ? nz : -1;
   const double bt = (double)L.best_t;
   DdaState d{L.gtx, L.gty, L.gtz, ix, iy, iz, false, false};
-  const DdaAxes ax{L.gdx, L.gdy, L.gdz, sx, sy, sz, ex, ey, ez};
+  const DdaAxes ax{(double)L.gdx, (double)L.gdy, (double)L.gdz, sx, sy, sz, ex, ey, ez};
   d = dda_step(d, ax, !stay, shadow, bt);
   // Cells of an empty macro-cell hold no object: walk through them here (the same steps and
   // end tests, no memory access) instead of spending a loop iteration and a load on each.  At most
@@ -1384,7 +1387,16 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   L.fl = fl;
 }
 
-template <bool STATS, int ACC>
+// Path-kernel modes whose shadow queries walk the 4-ary shadow tree (see the node loop).
+template <int MODE>
+constexpr bool kPathWide =
+#ifdef DRT_PATH_WIDE
+    MODE != MODE_SKEL;
+#else
+    MODE == MODE_REPLAY;
+#endif
+
+template <bool STATS, int ACC, int MODE>
 __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs& F, Lane& L,
                                              Counters& C) {  // main.cpp:386-422
   const int li = light_of_pair(L.j, F);
@@ -1399,11 +1411,8 @@ __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs
   if (ACC == ACC_GRID)  // Grid::Traverse(Ray&) gets the unit L: range |L|, direction re-normalised (Q1)
     start_query<STATS, ACC>(S, L, make_ray(so, normalize(Lv)), true, length(Lv), C);
   else  // BVH::Traverse(Ray&) normalises Ls and accepts t <= |Ls| + EPSILON (bvh.cpp:321-322, :376)
-#ifdef DRT_PATH_WIDE  // (A/B) shadow tree in the path kernel (see the node loop)
-    start_query<STATS, ACC, true>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
-#else
-    start_query<STATS, ACC>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)), C);
-#endif
+    start_query<STATS, ACC, kPathWide<MODE>>(S, L, make_ray(so, normalize(Ls)), true, shadow_threshold(length(Ls)),
+                                             C);
 }
 
 // reflectDir (main.cpp:504-508); MODE_SEQ draws rnd_unit_sphere on the lane's keyed stream
@@ -1412,6 +1421,7 @@ template <int MODE>
 __device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 V) {
   V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
   if (MODE == MODE_SEQ || MODE == MODE_PROG || MODE == MODE_SKEL || MODE == MODE_REPLAY) {
+    if (MODE == MODE_REPLAY && F.aa_chain) return normalize(R);  // an AA frame's replay: MODE_AA's reflection
     KRng rng{F.seed, L.pmix, L.rk};
     R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
     L.rk = rng.k;
@@ -1526,7 +1536,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
       L.lightPos = mk(0, 0, 0);
       L.j = 0;
       if (S.n_lights > 0) {
-        setup_shadow<STATS, ACC>(S, F, L, C);
+        setup_shadow<STATS, ACC, MODE>(S, F, L, C);
         return;
       }
       after_lights = true;
@@ -1535,7 +1545,7 @@ __device__ void lane_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Fr
     if (!hit) L.acc = add(L.acc, light_term(S.mats[L.mat], L.NdotL, L.NdotH, S.lights[light_of_pair(L.j, F)], F));
     L.j = next_light_pair(S, F, L.j);
     if (L.j < S.n_lights * F.light_spp) {
-      setup_shadow<STATS, ACC>(S, F, L, C);
+      setup_shadow<STATS, ACC, MODE>(S, F, L, C);
       return;
     }
     after_lights = true;
@@ -1697,6 +1707,30 @@ __device__ void skel_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Co
   L.item = kNoItem;
 }
 
+// MODE_CHAIN: the closest query of bounce L.depth of AA sample L.item returned: record it and go on
+// with the mirror child exactly as lane_process would (main.cpp:453-512; a two-pass scene has no
+// refraction), or end the item.  Shadow rays and colours are the replay pass's.
+template <bool STATS, int ACC>
+__device__ void chain_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
+  const bool hit = (L.fl & LF_HIT) != 0u;
+  F.skel_hits[(size_t)L.item * (uint32_t)(F.max_depth + 1) + (uint32_t)(L.depth - 1)] =
+      make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
+  if (hit && L.depth <= F.max_depth) {
+    const uint32_t mat = prim_material(S.prims[3 * L.best_prim]);
+    if (S.mats[mat].ks > 0.0f) {
+      const V3 hitP = add(L.q.o, mul(L.q.d, L.best_t));  // main.cpp:361
+      V3 N = normalize(prim_normal(S.prims, L.best_prim, L.q, L.best_t));
+      if (!(dot(L.q.d, N) < 0.0f)) N = neg(N);
+      const V3 V = neg(normalize(L.q.d));
+      const V3 R = reflect_dir<MODE_AA>(F, L, N, V);
+      L.depth++;
+      start_query<STATS, ACC>(S, L, make_ray(add(hitP, mul(N, 1e-4f)), R), false, 0.0f, C);
+      return;
+    }
+  }
+  L.item = kNoItem;
+}
+
 // MODE_SEQ: start sample L.smp of pixel L.item (path_kernel's in-order loop, main.cpp:651-665,
 // or the Whitted light-sample loop with glossy reflection, main.cpp:683-697).  The samples of
 // a pixel go to samples[pixel * nsub + smp]; the ordered reduce sums them as the loop did.
@@ -1775,7 +1809,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     }
     L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     L.smp = (uint32_t)it.sub;
-    L.rk = F.skel_rk[item];
+    L.rk = F.skel_rk ? F.skel_rk[item] : 0u;  // an AA frame's replay has no stream positions
     seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
     return;
   }
@@ -1812,7 +1846,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
   L.fl = 0u;
   if (STATS) C.v[ST_SAMPLES]++;
   RayP r;
-  if (MODE == MODE_AA) {
+  if (MODE == MODE_AA || MODE == MODE_CHAIN) {
     const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     float rx, ry, sx, sy;
     const int pos = F.perm ? (int)F.perm[item] : shuffle_source(F, pmix, it.sub);  // item = pixel * spp + sub
@@ -1990,7 +2024,8 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         // in the replay pass, whose register allocation it tips (VGPR spills 42 -> 96, C4 1 290 ->
         // 770 Mrays/s), and in one-pass in-order frames (scratch 2 464 -> 2 496 B); mixed-primitive
         // scenes keep the whole-leaf step (C2, balls_low: 23 000 -> 20 800 Mrays/s with it)
-        constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL ? 1 : 2);
+        constexpr int kLeaf1 =
+            !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
         // The shadow tree stays out of the path kernel (measured, round 4, headline 512^2 x 64 spp): its
         // lanes walked 26 % fewer node records per ray (75.8 -> 56.2 visits), but a wave whose lanes
         // mix closest-hit and shadow queries runs the binary and the 4-ary child tests one after the
@@ -1998,11 +2033,9 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         // 1 509 Mrays/s with it switched off in the same build, and the code compiled into the loop
         // cost 1 509 against 1 757 Mrays/s by itself (tools/lib_matrix.sh).  The
         // streaming shadow kernel, whose waves hold shadow queries only, uses it.
-#ifdef DRT_PATH_WIDE  // (A/B) shadow tree in the path kernel
-        constexpr bool kWide = MODE != MODE_SKEL;
-#else
-        constexpr bool kWide = false;
-#endif
+        // The replay pass of two-pass in-order frames reads its closest hits back, so every lane that
+        // traverses there holds a shadow query: its waves are homogeneous, as in the streaming kernel.
+        constexpr bool kWide = kPathWide<MODE>;
         if (in_trav)
           node_step<TRI_ONLY, STATS, CAP, 0, kLeaf1, kWide>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t, wave_finite, C,
                                                             cyc[3]);
@@ -2026,6 +2059,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
       if (done) {
         if (MODE == MODE_SEQ && part == kPartYield) L.fl |= LF_YIELD;
         if constexpr (MODE == MODE_SKEL) skel_process<STATS, ACC>(S, F, L, C);
+        else if constexpr (MODE == MODE_CHAIN) chain_process<STATS, ACC>(S, F, L, C);
         else lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
       }
     }
@@ -2342,6 +2376,7 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
     case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ, A>(S, F, st); break;
     case MODE_SKEL: launch_persistent_m<T, ST, MODE_SKEL, A>(S, F, st); break;
     case MODE_REPLAY: launch_persistent_m<T, ST, MODE_REPLAY, A>(S, F, st); break;
+    case MODE_CHAIN: launch_persistent_m<T, ST, MODE_CHAIN, A>(S, F, st); break;
     case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG, A>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT, A>(S, F, st); break;
   }

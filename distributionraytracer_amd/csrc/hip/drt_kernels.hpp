@@ -19,9 +19,13 @@ enum FrameMode : int {
   MODE_SKEL = 5,    // pass 1, one lane per pixel, samples in order: only the closest-hit chain of
                     // each sample (primary ray, mirror bounces) — which fixes every random draw's
                     // position — recording each sample's stream position and each bounce's hit
-  MODE_REPLAY = 6   // pass 2, one lane per (pixel, sample), any order: the whole rayTracing() of
+  MODE_REPLAY = 6,  // pass 2, one lane per (pixel, sample), any order: the whole rayTracing() of
                     // the sample from its recorded stream position, closest hits read back, shadow
                     // rays traced
+  // An AA frame (MODE_AA) of a refraction-free BVH scene in two passes (round 4), so that the
+  // shadow queries run in waves of shadow queries only, on the 4-ary shadow tree:
+  MODE_CHAIN = 7    // pass 1, one lane per (pixel, sample): the sample's closest-hit chain only,
+                    // each bounce's hit recorded; pass 2 is MODE_REPLAY
 };
 
 enum StatSlot : int {
@@ -148,6 +152,9 @@ struct FrameArgs {
   // bounce: (t bits, primitive record), primitive 0xFFFFFFFF = miss
   uint32_t* skel_rk;
   uint2* skel_hits;
+  // MODE_REPLAY of an AA frame (pass 2 after MODE_CHAIN): no keyed-stream positions (skel_rk null);
+  // reflections use MODE_AA's direction (the draws after the prologue never reach the frame, Q16)
+  int aa_chain;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

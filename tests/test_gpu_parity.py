@@ -64,11 +64,26 @@ def assert_same_work(accel, st, rst):
 
 
 def assert_same_work_frame(renderer, img, rst, seed, **kw):
-    """Re-render a frame with the kernel's stats build: the same frame bit for bit, and the
-    oracle's traversal work (assert_same_work)."""
-    img_s = renderer.render(seed=seed, stats=True, **kw)
+    """Re-render a frame with the kernel's stats build in the reference's traversal order
+    (DRT_FRAME_REFERENCE_ORDER: one pass, every shadow query on the reference's binary tree): the
+    same frame bit for bit as `img` (the default frame: AA and in-order BVH frames in two passes,
+    their replay pass's shadow queries on the 4-ary shadow tree), and the oracle's traversal work
+    (assert_same_work)."""
+    img_s = renderer.render(seed=seed, stats=True, reference_order=True, **kw)
     np.testing.assert_array_equal(bits(img_s), bits(img))
     assert_same_work(renderer.scene.info().accel, renderer.stats(), rst)
+
+
+def assert_default_frame_work(accel, st, rst):
+    """A default frame: every ray counted and the closest-hit work equal to the oracle's; shadow
+    queries may have walked the 4-ary shadow tree (counted in the wide_* fields)."""
+    if accel == 0:
+        return
+    assert st["closest_rays"] == rst["closest_calls"] and st["shadow_rays"] == rst["shadow_calls"]
+    for k in ("closest_leaf", "closest_prims") + (("closest_inner",) if accel == 2 else ()):
+        assert st[k] == rst[k], (k, st[k], rst[k])
+    if st["wide_shadow_rays"] == 0:
+        assert_same_work(accel, st, rst)
 
 
 GOLD_CASES = ["tiny", "mixed", "tris2k"]
@@ -191,9 +206,12 @@ def test_render_matches_oracle(drt, oracle_mod, renderer, tmp_path, case):
     st = renderer.stats()
     ref, rst = b.render(seed=seed, **kw)
     compare_images(img, ref)
-    # identical branching => identical traversal work
-    assert_same_work(a.info().accel, st, rst)
+    assert_default_frame_work(a.info().accel, st, rst)
     assert st["samples"] == rst["samples"]
+    # the reference's traversal order: the same frame bit for bit, identical traversal work
+    img_r = renderer.render(seed=seed, stats=True, reference_order=True, **kw)
+    np.testing.assert_array_equal(bits(img_r), bits(img))
+    assert_same_work(a.info().accel, renderer.stats(), rst)
 
 
 @pytest.mark.parametrize("accel,aperture,roughness", [("bvh", 0.0, 0.0), ("bvh", 8.0, 0.2), ("grid", 0.0, 0.0),
@@ -744,6 +762,39 @@ def test_slot_reused_from_another_stream_waits_for_its_last_frame(drt, renderer,
         np.testing.assert_array_equal(outs[i].cpu().numpy().view(np.uint32), lone[i].view(np.uint32), err_msg=str(i))
 
 
+@pytest.mark.parametrize("kw", [{}, {"light_spp": 4}, {"max_depth": 8}])
+def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, kw):
+    """AA frames of refraction-free BVH scenes run in two passes (round 4; drt_capi.hip plan,
+    FrameMode MODE_CHAIN / MODE_REPLAY): the samples' closest-hit chains, then every sample's shading
+    with its closest hits read back, whose shadow queries walk the 4-ary shadow tree.  The frame
+    equals the one-pass AA frame (DRT_AA_TWO_PASS=0) and the reference-order frame bit for bit, with
+    the same rays and closest-hit work; the reference-order frame is one pass with the reference's
+    shadow work."""
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(50_000), 64, 16)
+    s.build()
+    renderer.upload(s)
+    assert renderer.plan(renderer.frame_params(seed=6, **kw))["passes"] == 2
+    assert renderer.plan(renderer.frame_params(seed=6, reference_order=True, **kw))["passes"] == 1
+    img = renderer.render(seed=6, stats=True, **kw)
+    st = renderer.stats()
+    assert st["wide_shadow_rays"] > 0.99 * st["shadow_rays"]
+    monkeypatch.setenv("DRT_AA_TWO_PASS", "0")
+    assert renderer.plan(renderer.frame_params(seed=6, **kw))["passes"] == 1
+    one = renderer.render(seed=6, stats=True, **kw)
+    st1 = renderer.stats()
+    ref = renderer.render(seed=6, stats=True, reference_order=True, **kw)
+    rst = renderer.stats()
+    np.testing.assert_array_equal(bits(img), bits(one))
+    np.testing.assert_array_equal(bits(img), bits(ref))
+    for k in ("closest_rays", "shadow_rays", "closest_inner", "closest_leaf", "closest_prims", "samples"):
+        assert st[k] == st1[k] == rst[k], k
+    for k in ("shadow_inner", "shadow_leaf", "shadow_prims"):
+        assert st1[k] == rst[k], k
+
+
 @pytest.mark.parametrize("accel,spp,kw", [("bvh", 16, {"roughness": 0.1, "max_depth": 8}), ("grid", 9, {"roughness": 0.2}),
                                           ("bvh", 0, {"roughness": 0.2})])
 def test_two_pass_in_order_frame_equals_one_pass(drt, renderer, tmp_path, monkeypatch, accel, spp, kw):
@@ -768,13 +819,15 @@ def test_two_pass_in_order_frame_equals_one_pass(drt, renderer, tmp_path, monkey
         s = drt.Scene.load_p3f(sg.write(tmp_path, "s.p3f", text))
     renderer.upload(s)
     assert renderer.plan(renderer.frame_params(seed=5, **kw))["passes"] == 2
-    img = renderer.render(seed=5, stats=True, **kw)
+    img = renderer.render(seed=5, **kw)  # the replay pass's shadow queries on the shadow tree (BVH)
+    img_r = renderer.render(seed=5, stats=True, reference_order=True, **kw)
     st = renderer.stats()
     monkeypatch.setenv("DRT_SEQ_TWO_PASS", "0")
     assert renderer.plan(renderer.frame_params(seed=5, **kw))["passes"] == 1
-    ref = renderer.render(seed=5, stats=True, **kw)
+    ref = renderer.render(seed=5, stats=True, reference_order=True, **kw)
     rst = renderer.stats()
     np.testing.assert_array_equal(bits(img), bits(ref))
+    np.testing.assert_array_equal(bits(img_r), bits(ref))
     for k in ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
               "closest_prims", "shadow_prims", "samples",
             "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify"):

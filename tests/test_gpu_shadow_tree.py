@@ -136,23 +136,3 @@ def test_shadow_tree_matches_oracle_on_mixed_primitives(drt, oracle_mod, rendere
     np.testing.assert_array_equal(wide, b.trace_shadow(rays))
     assert st_w["wide_shadow_rays"] > 0 and st_w["shadow_rays"] == len(rays)
     assert st_w["wide_shadow_rays"] < len(rays)  # the non-finite rays keep the reference's tree
-
-
-def test_frames_render_every_shadow_query_on_the_reference_tree(drt, renderer):
-    """The path kernel walks shadow queries on the reference's tree (the shadow tree measured slower
-    there): frame stats count no shadow-tree work, with or without the frame flag."""
-    import bench
-
-    s = drt.Scene()
-    bench.populate(s, bench.synthetic_triangles(20_000), 48, 4)
-    s.build()
-    renderer.upload(s)
-    a = renderer.render(seed=4, stats=True)
-    st = renderer.stats()
-    b = renderer.render(seed=4, stats=True, reference_order=True)
-    assert st["wide_shadow_rays"] == 0 and st["shadow_rays"] > 0
-    st_r = renderer.stats()
-    for k in ("closest_rays", "shadow_rays", "closest_inner", "shadow_inner", "closest_leaf", "shadow_leaf",
-              "closest_prims", "shadow_prims", "wide_shadow_rays", "wide_inner", "wide_prims"):
-        assert st[k] == st_r[k], k
-    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
