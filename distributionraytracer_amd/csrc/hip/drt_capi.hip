@@ -1047,6 +1047,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F1.skel_rk = P.aa_chain ? nullptr : d_rk.as<uint32_t>();
     F1.skel_hits = d_hits.as<uint2>();
     F1.aa_chain = P.aa_chain ? 1 : 0;
+    if (P.aa_chain) F1.waves = env_int("DRT_CHAIN_WAVES", 6);  // the closest-chain pass carries little state
     F1.seq_cont = nullptr;
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());

@@ -1216,15 +1216,17 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       tn[k] = t0;
     }
 #endif
-    // go on with the hit child entered first (any order gives the same answer); push the others
+    // go on with the first hit child (any order gives the same answer); push the others.  Nearest-
+    // first order (the reference's rule for its two children) measured 1.6 % / 3.1 % slower on the
+    // headline / C3 replay pass than this first-hit order (profiles/r04_replay_tuning_ab.jsonl).
     int ci = -1;
     float best = 0.0f;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-#ifdef DRT_WIDE_FIRST  // (A/B) the first hit child, no distance order
-      const bool take = hk[k] && ci < 0;
-#else
+#ifdef DRT_WIDE_NEAREST  // (A/B) the hit child entered first
       const bool take = hk[k] && (ci < 0 || tn[k] < best);
+#else
+      const bool take = hk[k] && ci < 0;
 #endif
       ci = take ? k : ci;
       best = take ? tn[k] : best;
@@ -2024,8 +2026,12 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         // in the replay pass, whose register allocation it tips (VGPR spills 42 -> 96, C4 1 290 ->
         // 770 Mrays/s), and in one-pass in-order frames (scratch 2 464 -> 2 496 B); mixed-primitive
         // scenes keep the whole-leaf step (C2, balls_low: 23 000 -> 20 800 Mrays/s with it)
+#ifdef DRT_REPLAY_LEAF1  // (A/B) one primitive per step in the replay pass too
+        constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
+#else
         constexpr int kLeaf1 =
             !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
+#endif
         // The shadow tree stays out of the path kernel (measured, round 4, headline 512^2 x 64 spp): its
         // lanes walked 26 % fewer node records per ray (75.8 -> 56.2 visits), but a wave whose lanes
         // mix closest-hit and shadow queries runs the binary and the 4-ary child tests one after the
