@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from tests import shipped
-from tests.test_gpu_parity import TOL, assert_same_work, compare_images
+from tests.test_gpu_parity import TOL, assert_default_frame_work, assert_same_work, bits, compare_images
 
 pytestmark = pytest.mark.gpu
 
@@ -68,8 +68,12 @@ def test_shipped_scene_matches_oracle(drt, oracle_mod, renderer, tmp_path, case)
     ref, rst = b.render(seed=2718, **kw)
     exact = compare_images(img, ref, TOL)
     assert exact > 0.5, f"only {exact:.3f} of the channels are bit-identical"
-    assert_same_work(a.info().accel, st, rst)
+    assert_default_frame_work(a.info().accel, st, rst)
     assert st["samples"] == rst["samples"]
+    # the reference's traversal order: the same frame bit for bit, the oracle's traversal work
+    img_r = renderer.render(seed=2718, stats=True, reference_order=True, **kw)
+    np.testing.assert_array_equal(bits(img_r), bits(img))
+    assert_same_work(a.info().accel, renderer.stats(), rst)
     if shipped.env(name):  # the sky, not bclr, fills the misses
         assert a.info().skybox_loaded
 

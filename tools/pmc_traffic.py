@@ -115,11 +115,11 @@ def main():
             continue
         kernel = k[1]
         cur = dict(c[k])
-        # a two-pass in-order frame (FrameMode 5 then 6, drt_capi.hip): the frame is both launches
+        # a two-pass frame (FrameMode 5 or 7, then 6, drt_capi.hip): the frame is both launches
         if _mode(k[1]) == 6:
-            prev = [d for d in c if d[0] < k[0] and _mode(d[1]) == 5 and not _stats(d[1])]
+            prev = [d for d in c if d[0] < k[0] and _mode(d[1]) in (5, 7) and not _stats(d[1])]
             if prev:
-                p5 = max(prev)
+                p5 = max(prev)  # the frame's first pass
                 kernel = p5[1] + " + " + k[1]
                 for n, v in c[p5].items():
                     cur[n] = cur.get(n, 0.0) + v
