@@ -1047,13 +1047,23 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F1.skel_rk = P.aa_chain ? nullptr : d_rk.as<uint32_t>();
     F1.skel_hits = d_hits.as<uint2>();
     F1.aa_chain = P.aa_chain ? 1 : 0;
-    if (P.aa_chain) F1.waves = env_int("DRT_CHAIN_WAVES", 6);  // the closest-chain pass carries little state
+    if (P.aa_chain) {  // the closest-chain pass carries little state
+      // its "shading" is recording a hit and starting the mirror ray: batches of 8 ready lanes
+      // measured 1 927 against 1 897 Mrays/s for 24 (1: 1 842, 48: 1 725; profiles/r04_pass_knobs_ab.jsonl)
+      F1.waves = env_int("DRT_CHAIN_WAVES", 6);  // 7 measured 1 785
+      F1.process_min = env_int("DRT_CHAIN_PROCESS_MIN", 8);
+      F1.refill_min = env_int("DRT_CHAIN_REFILL_MIN", P.F.refill_min);  // 16 measured 1 868
+    } else {
+      F1.process_min = env_int("DRT_SKEL_PROCESS_MIN", P.F.process_min);
+    }
     F1.seq_cont = nullptr;
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
     F2.mode = MODE_REPLAY;
-    F2.waves = P.F.waves;
+    F2.waves = env_int("DRT_REPLAY_WAVES", P.F.waves);
+    F2.process_min = env_int("DRT_REPLAY_PROCESS_MIN", P.F.process_min);  // 12 / 40: 1 861 / 1 764 vs 1 897
+    F2.refill_min = env_int("DRT_REPLAY_REFILL_MIN", P.F.refill_min);
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));
