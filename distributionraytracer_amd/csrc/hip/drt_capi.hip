@@ -893,8 +893,12 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // wave mix both query kinds and the shadow tree measured slower.  Same conditions
   // as above (no refraction, the record fits), a BVH with its shadow tree, and not a reference-order
   // frame (DRT_FRAME_REFERENCE_ORDER keeps the one-pass frame); DRT_AA_TWO_PASS=0 keeps one pass.
+  // Scenes of few objects keep one pass too: their traversal is short, so the pass boundary costs
+  // more than the shadow tree saves (C2, balls_low's 11 objects: 17 500 against 23 300 Mrays/s in two
+  // passes; DRT_AA_TWO_PASS_MIN_PRIMS, default 1024).
   P.aa_chain = false;
   if (P.persistent && F.mode == MODE_AA && c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide &&
+      c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) &&
       !(p->flags & DRT_FRAME_REFERENCE_ORDER) && env_int("DRT_AA_TWO_PASS", 1) != 0 &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
     bool refr = false;
