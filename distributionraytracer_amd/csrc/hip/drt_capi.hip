@@ -257,6 +257,7 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
     int depth;
   };
   std::vector<Item> st{{0u, 0u, 1}};
+  const int order = env_int("DRT_WIDE_ORDER", 2);
   out.emplace_back();
   int maxd = 1;
   while (!st.empty()) {
@@ -279,6 +280,14 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
       const uint32_t c = ch[best];
       ch[best] = nodes[c].index;
       ch[n++] = nodes[c].index + 1;
+    }
+    // child slot order: the device enters the first hit slot, then the others in slot order.  Default
+    // 2, ascending box surface (0: as collapsed, 1: descending, 3: leaves first, then descending)
+    if (order == 1 || order == 2 || order == 3) {
+      std::stable_sort(ch, ch + n, [&](uint32_t a, uint32_t b) {
+        if (order == 3 && nodes[a].leaf != nodes[b].leaf) return nodes[a].leaf > nodes[b].leaf;
+        return order == 2 ? area(a) < area(b) : area(a) > area(b);
+      });
     }
     WideNodeRecord r{};
     for (int a = 0; a < 3; a++) {
@@ -897,7 +906,10 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // more than the shadow tree saves (C2, balls_low's 11 objects: 17 500 against 23 300 Mrays/s in two
   // passes; DRT_AA_TWO_PASS_MIN_PRIMS, default 1024).
   P.aa_chain = false;
-  if (P.persistent && F.mode == MODE_AA && c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide &&
+  // The Grid's AA frames too (its shadow queries stay on the Grid: Grid::Traverse(Ray&)'s answer is
+  // tied to the cells its walk visits): 1 381 against 1 295 Mrays/s on the Grid headline scene.
+  const bool grid_chain = c->accel == DRT_ACCEL_GRID && c->has_grid && env_int("DRT_AA_TWO_PASS_GRID", 1) != 0;
+  if (P.persistent && F.mode == MODE_AA && (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) &&
       !(p->flags & DRT_FRAME_REFERENCE_ORDER) && env_int("DRT_AA_TWO_PASS", 1) != 0 &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
@@ -1054,7 +1066,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     if (P.aa_chain) {  // the closest-chain pass carries little state
       // its "shading" is recording a hit and starting the mirror ray: batches of 8 ready lanes
       // measured 1 927 against 1 897 Mrays/s for 24 (1: 1 842, 48: 1 725; profiles/r04_pass_knobs_ab.jsonl)
-      F1.waves = env_int("DRT_CHAIN_WAVES", 6);  // 7 measured 1 785
+      // (Grid: 5 waves, 1 381 against 1 318 Mrays/s at 6 on the Grid headline scene;
+      // profiles/r04_grid_two_pass_wide_order_ab.jsonl)
+      F1.waves = env_int("DRT_CHAIN_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 6);  // BVH: 7 measured 1 785
       F1.process_min = env_int("DRT_CHAIN_PROCESS_MIN", 8);
       F1.refill_min = env_int("DRT_CHAIN_REFILL_MIN", P.F.refill_min);  // 16 measured 1 868
     } else {

@@ -1233,8 +1233,13 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     }
     constexpr uint32_t kWideLds = 2u * kLdsBytes;  // a shadow-tree stack uses the t rows too
     uint32_t spa = L.spa;
+    // pushed in reverse, so that the pops go on in slot order: with the slots in ascending box
+    // surface (build_wide, DRT_WIDE_ORDER 2) a lane enters its hit children smallest first.  Measured
+    // on the headline: 1 956 against 1 929-1 931 Mrays/s for the build order with pushes in slot
+    // order; 1 947 with ascending slots pushed in slot order, 1 951-1 953 descending and reversed
+    // (profiles/r04_wide_order_push_ab.jsonl).
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 3; k >= 0; k--) {
       if (hk[k] && k != ci) {
         if (spa < kWideLds) *(LdsU32*)(lds + spa) = d[k];
         else ov_desc[(spa - kWideLds) >> kRowShift] = d[k];
@@ -2378,6 +2383,12 @@ static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStrea
   }
   // (MODE_SKEL, the closest-chain pass, carries little state: 4 spills at 6 waves.  Measured at 4, 5,
   // 7 and 8 waves/SIMD on C4: 305, 280, 554 and 760 ms against 278 ms at 6.)
+#ifdef DRT_REPLAY_LOW_WAVES
+  if constexpr (M == MODE_REPLAY) {
+    if (F.waves == 5) return launch_persistent_w<T, ST, M, 5, A>(S, F, st);
+    if (F.waves == 4) return launch_persistent_w<T, ST, M, 4, A>(S, F, st);
+  }
+#endif
   if (F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);
   else launch_persistent_w<T, ST, M, 6, A>(S, F, st);
 }

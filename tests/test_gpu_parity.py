@@ -762,26 +762,31 @@ def test_slot_reused_from_another_stream_waits_for_its_last_frame(drt, renderer,
         np.testing.assert_array_equal(outs[i].cpu().numpy().view(np.uint32), lone[i].view(np.uint32), err_msg=str(i))
 
 
-@pytest.mark.parametrize("kw", [{}, {"light_spp": 4}, {"max_depth": 8}])
-def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, kw):
-    """AA frames of refraction-free BVH scenes run in two passes (round 4; drt_capi.hip plan,
-    FrameMode MODE_CHAIN / MODE_REPLAY): the samples' closest-hit chains, then every sample's shading
-    with its closest hits read back, whose shadow queries walk the 4-ary shadow tree.  The frame
-    equals the one-pass AA frame (DRT_AA_TWO_PASS=0) and the reference-order frame bit for bit, with
-    the same rays and closest-hit work; the reference-order frame is one pass with the reference's
-    shadow work."""
+@pytest.mark.parametrize("accel,kw", [("bvh", {}), ("bvh", {"light_spp": 4}), ("bvh", {"max_depth": 8}),
+                                      ("grid", {}), ("grid", {"light_spp": 4, "max_depth": 8})])
+def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, accel, kw):
+    """AA frames of refraction-free BVH and Grid scenes run in two passes (round 4; drt_capi.hip
+    plan, FrameMode MODE_CHAIN / MODE_REPLAY): the samples' closest-hit chains, then every sample's
+    shading with its closest hits read back, whose shadow queries walk the 4-ary shadow tree (BVH) or
+    the Grid.  The frame equals the one-pass AA frame (DRT_AA_TWO_PASS=0 / DRT_AA_TWO_PASS_GRID=0)
+    and the reference-order frame bit for bit, with the same rays and closest-hit work; the
+    reference-order frame is one pass with the reference's shadow work (on the Grid every count is
+    the same in all three frames)."""
     import bench
 
     s = drt.Scene()
-    bench.populate(s, bench.synthetic_triangles(50_000), 64, 16)
+    bench.populate(s, bench.synthetic_triangles(50_000), 64, 16, accel=accel)
     s.build()
     renderer.upload(s)
     assert renderer.plan(renderer.frame_params(seed=6, **kw))["passes"] == 2
     assert renderer.plan(renderer.frame_params(seed=6, reference_order=True, **kw))["passes"] == 1
     img = renderer.render(seed=6, stats=True, **kw)
     st = renderer.stats()
-    assert st["wide_shadow_rays"] > 0.99 * st["shadow_rays"]
-    monkeypatch.setenv("DRT_AA_TWO_PASS", "0")
+    if accel == "bvh":
+        assert st["wide_shadow_rays"] > 0.99 * st["shadow_rays"]
+    else:
+        assert st["wide_shadow_rays"] == 0
+    monkeypatch.setenv("DRT_AA_TWO_PASS_GRID" if accel == "grid" else "DRT_AA_TWO_PASS", "0")
     assert renderer.plan(renderer.frame_params(seed=6, **kw))["passes"] == 1
     one = renderer.render(seed=6, stats=True, **kw)
     st1 = renderer.stats()
@@ -789,7 +794,10 @@ def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, kw):
     rst = renderer.stats()
     np.testing.assert_array_equal(bits(img), bits(one))
     np.testing.assert_array_equal(bits(img), bits(ref))
-    for k in ("closest_rays", "shadow_rays", "closest_inner", "closest_leaf", "closest_prims", "samples"):
+    keys = ["closest_rays", "shadow_rays", "closest_inner", "closest_leaf", "closest_prims", "samples"]
+    if accel == "grid":
+        keys += ["shadow_inner", "shadow_leaf", "shadow_prims"]
+    for k in keys:
         assert st[k] == st1[k] == rst[k], k
     for k in ("shadow_inner", "shadow_leaf", "shadow_prims"):
         assert st1[k] == rst[k], k
