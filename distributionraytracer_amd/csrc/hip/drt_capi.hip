@@ -1071,6 +1071,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       F1.waves = env_int("DRT_CHAIN_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 6);  // BVH: 7 measured 1 785
       F1.process_min = env_int("DRT_CHAIN_PROCESS_MIN", 8);
       F1.refill_min = env_int("DRT_CHAIN_REFILL_MIN", P.F.refill_min);  // 16 measured 1 868
+      // Grid: 3 empty cells per call in both passes of an AA two-pass frame (1 420 against 1 383 Mrays/s
+      // at the one-pass frame's 5; 2: 1 413; profiles/r04_hit_normals_grid_walk_ab.jsonl)
+      F1.grid_walk = std::max(0, env_int("DRT_CHAIN_GRID_WALK", 3));
+      F1.grid_pairs = std::max(1, env_int("DRT_CHAIN_GRID_PAIRS", P.F.grid_pairs));
     } else {
       F1.process_min = env_int("DRT_SKEL_PROCESS_MIN", P.F.process_min);
     }
@@ -1082,6 +1086,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F2.waves = env_int("DRT_REPLAY_WAVES", P.F.waves);
     F2.process_min = env_int("DRT_REPLAY_PROCESS_MIN", P.F.process_min);  // 12 / 40: 1 861 / 1 764 vs 1 897
     F2.refill_min = env_int("DRT_REPLAY_REFILL_MIN", P.F.refill_min);
+    F2.grid_walk = std::max(0, env_int("DRT_REPLAY_GRID_WALK", P.aa_chain ? 3 : P.F.grid_walk));
+    F2.grid_pairs = std::max(1, env_int("DRT_REPLAY_GRID_PAIRS", P.F.grid_pairs));
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));
