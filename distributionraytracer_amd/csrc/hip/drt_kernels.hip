@@ -2377,10 +2377,8 @@ static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStrea
   // walk is capped per call (round 2: 1 101-1 177 against 1 039-1 085 at 6, interleaved runs;
   // 4 waves 983, 7 waves 880)
   if (A == ACC_GRID) {
-#ifdef DRT_GRID_CHAIN_W4
-    if constexpr (M == MODE_CHAIN)
-      if (F.waves == 4) return launch_persistent_w<T, ST, M, 4, A>(S, F, st);
-#endif
+    // (the Grid's closest-chain pass: 5 waves; 4 measured 1 364-1 369 against 1 424-1 427 Mrays/s,
+    // 6 measured 1 318 against 1 381, profiles/r04_grid_chain_waves_ab.jsonl)
     if (F.waves == 6) launch_persistent_w<T, ST, M, 6, A>(S, F, st);
     else launch_persistent_w<T, ST, M, 5, A>(S, F, st);
     return;
