@@ -1027,8 +1027,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   DRT_HIP(c, hipEventRecord(ev[0], st));
   const bool persistent = P.persistent;
   if (persistent) {
-    DRT_HIP(c, d_counter.ensure(1024));
-    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));  // 8 partition counters, 64 B apart
+    // 8 partition counters, 64 B apart, per pass: a two-pass frame's second pass uses the second
+    // KiB, zeroed here too, so that no fill kernel sits between the passes (a fill waits for a CU
+    // slot behind the other frames' persistent blocks, and the second pass behind it)
+    DRT_HIP(c, d_counter.ensure(2048));
+    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, P.two_pass ? 2048 : 1024, st));
     P.F.work_counter = d_counter.as<unsigned int>();
     P.F.part_items = (uint32_t)((P.F.n_items + 7) / 8);
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
@@ -1090,7 +1093,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F2.grid_pairs = std::max(1, env_int("DRT_REPLAY_GRID_PAIRS", P.F.grid_pairs));
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
-    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, 1024, st));
+    F2.work_counter = d_counter.as<unsigned int>() + 256;
     launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
   } else if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
