@@ -906,10 +906,18 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // more than the shadow tree saves (C2, balls_low's 11 objects: 17 500 against 23 300 Mrays/s in two
   // passes; DRT_AA_TWO_PASS_MIN_PRIMS, default 1024).
   P.aa_chain = false;
+  // Small frames keep one pass too: each pass ends in a tail where most CUs wait for the last lanes,
+  // and the second pass adds ~0.5 ms to a frame rendered alone (shipped dragon scene, 800x600 x 16
+  // spp, 7.7 M samples: 2.72 / 2.15 ms Grid / BVH in two passes against 2.02 / 1.63 in one;
+  // balls_high 512^2 x 16: BVH 5.21 against 4.79 ms; profiles/r04_two_pass_small_frames_ab.txt).  The
+  // threshold counts the whole frame's samples (RES_X x RES_Y x spp), so a tile shard of a large
+  // frame keeps the two-pass plan of the whole frame (N = 8: 11.5 against 12.4 ms per shard).
+  const uint64_t frame_samples = (uint64_t)RX * (uint64_t)RY * (uint64_t)std::max(1, (int)c->spp);
+  const bool big_frame = frame_samples >= (uint64_t)std::max(0, env_int("DRT_AA_TWO_PASS_MIN_SAMPLES", 1 << 23));
   // The Grid's AA frames too (its shadow queries stay on the Grid: Grid::Traverse(Ray&)'s answer is
   // tied to the cells its walk visits): 1 381 against 1 295 Mrays/s on the Grid headline scene.
   const bool grid_chain = c->accel == DRT_ACCEL_GRID && c->has_grid && env_int("DRT_AA_TWO_PASS_GRID", 1) != 0;
-  if (P.persistent && F.mode == MODE_AA && (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
+  if (P.persistent && F.mode == MODE_AA && big_frame && (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) &&
       !(p->flags & DRT_FRAME_REFERENCE_ORDER) && env_int("DRT_AA_TWO_PASS", 1) != 0 &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {

@@ -803,6 +803,28 @@ def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, accel, kw
         assert st1[k] == rst[k], k
 
 
+@pytest.mark.parametrize("accel", ["bvh", "grid"])
+def test_aa_two_pass_sample_threshold(drt, renderer, monkeypatch, accel):
+    """Small AA frames keep one pass (the second pass's tail costs ~0.5 ms per frame rendered alone):
+    the plan counts the whole frame's samples against DRT_AA_TWO_PASS_MIN_SAMPLES (default 2^23).  A
+    64 x 64 x 16 frame has 65 536 samples; both plans render the same frame."""
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(20_000), 64, 16, accel=accel)
+    s.build()
+    renderer.upload(s)
+    monkeypatch.delenv("DRT_AA_TWO_PASS_MIN_SAMPLES")
+    assert renderer.plan(renderer.frame_params(seed=3))["passes"] == 1
+    one = renderer.render(seed=3)
+    monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_SAMPLES", "65536")
+    assert renderer.plan(renderer.frame_params(seed=3))["passes"] == 2
+    two = renderer.render(seed=3)
+    monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_SAMPLES", "65537")
+    assert renderer.plan(renderer.frame_params(seed=3))["passes"] == 1
+    np.testing.assert_array_equal(bits(one), bits(two))
+
+
 @pytest.mark.parametrize("accel,spp,kw", [("bvh", 16, {"roughness": 0.1, "max_depth": 8}), ("grid", 9, {"roughness": 0.2}),
                                           ("bvh", 0, {"roughness": 0.2})])
 def test_two_pass_in_order_frame_equals_one_pass(drt, renderer, tmp_path, monkeypatch, accel, spp, kw):

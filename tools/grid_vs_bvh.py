@@ -60,11 +60,15 @@ def measure(r, tmp, name, accel, spp, frames):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=30)
+    ap.add_argument("--scenes", default=",".join(SCENES))
+    ap.add_argument("--modes", default="whitted,aa16")
     args = ap.parse_args()
     r = drt.Renderer(0)
     with tempfile.TemporaryDirectory() as tmp:
-        for name in SCENES:
+        for name in args.scenes.split(","):
             for mode, spp in (("whitted", None), ("aa16", 16)):
+                if mode not in args.modes.split(","):
+                    continue
                 g, gi = measure(r, tmp, name, "grid", spp, args.frames)
                 b, bi = measure(r, tmp, name, "bvh", spp, args.frames)
                 # the two accelerators' frames agree (tie-breaking between equal-t objects may differ)
