@@ -163,6 +163,10 @@ static int env_int(const char* name, int dflt) {  // tuning knobs for A/B runs
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }
+static double env_double(const char* name, double dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atof(v) : dflt;
+}
 
 static PrimRecord pack_prim(const drt_prim& p, uint32_t mat, uint32_t obj) {
   PrimRecord r{};
@@ -818,6 +822,7 @@ struct Plan {
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
 
+static void note_last_path_ms(drt_ctx* c);
 static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
   const int shards = p->n_shards <= 0 ? 1 : p->n_shards;
@@ -906,14 +911,16 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // more than the shadow tree saves (C2, balls_low's 11 objects: 17 500 against 23 300 Mrays/s in two
   // passes; DRT_AA_TWO_PASS_MIN_PRIMS, default 1024).
   P.aa_chain = false;
-  // Small frames keep one pass too: each pass ends in a tail where most CUs wait for the last lanes,
+  // Short frames keep one pass too: each pass ends in a tail where most CUs wait for the last lanes,
   // and the second pass adds ~0.5 ms to a frame rendered alone (shipped dragon scene, 800x600 x 16
-  // spp, 7.7 M samples: 2.72 / 2.15 ms Grid / BVH in two passes against 2.02 / 1.63 in one;
-  // balls_high 512^2 x 16: BVH 5.21 against 4.79 ms; profiles/r04_two_pass_small_frames_ab.txt).  The
-  // threshold counts the whole frame's samples (RES_X x RES_Y x spp), so a tile shard of a large
-  // frame keeps the two-pass plan of the whole frame (N = 8: 11.5 against 12.4 ms per shard).
-  const uint64_t frame_samples = (uint64_t)RX * (uint64_t)RY * (uint64_t)std::max(1, (int)c->spp);
-  const bool big_frame = frame_samples >= (uint64_t)std::max(0, env_int("DRT_AA_TWO_PASS_MIN_SAMPLES", 1 << 23));
+  // spp: 2.72 / 2.15 ms Grid / BVH in two passes against 2.02 / 1.63 in one; balls_high 512^2 x 16:
+  // BVH 5.21 against 4.79 ms), while longer frames gain (the 1M-triangle scene at 512^2 x 16 spp:
+  // 22.3 against 24.3 ms; profiles/r04_two_pass_small_frames_ab.txt, r04_two_pass_frame_time_ab.jsonl).
+  // The context's newest completed frame decides, as for the auxiliary streams: two passes while no
+  // frame has completed or the last one's path kernels took >= DRT_AA_TWO_PASS_MIN_MS (default 6 ms).
+  // Both plans render the same frame.
+  note_last_path_ms(c);
+  const bool big_frame = c->last_path_ms < 0.0 || c->last_path_ms >= env_double("DRT_AA_TWO_PASS_MIN_MS", 6.0);
   // The Grid's AA frames too (its shadow queries stay on the Grid: Grid::Traverse(Ray&)'s answer is
   // tied to the cells its walk visits): 1 381 against 1 295 Mrays/s on the Grid headline scene.
   const bool grid_chain = c->accel == DRT_ACCEL_GRID && c->has_grid && env_int("DRT_AA_TWO_PASS_GRID", 1) != 0;

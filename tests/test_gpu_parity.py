@@ -804,25 +804,28 @@ def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, accel, kw
 
 
 @pytest.mark.parametrize("accel", ["bvh", "grid"])
-def test_aa_two_pass_sample_threshold(drt, renderer, monkeypatch, accel):
-    """Small AA frames keep one pass (the second pass's tail costs ~0.5 ms per frame rendered alone):
-    the plan counts the whole frame's samples against DRT_AA_TWO_PASS_MIN_SAMPLES (default 2^23).  A
-    64 x 64 x 16 frame has 65 536 samples; both plans render the same frame."""
+def test_aa_two_pass_frame_time_rule(drt, monkeypatch, accel):
+    """Short AA frames keep one pass (the second pass's tail costs ~0.5 ms per frame rendered alone):
+    a context plans two passes while none of its frames has completed or its newest completed frame
+    took >= DRT_AA_TWO_PASS_MIN_MS (default 6 ms).  Both plans render the same frame."""
     import bench
 
     s = drt.Scene()
     bench.populate(s, bench.synthetic_triangles(20_000), 64, 16, accel=accel)
     s.build()
-    renderer.upload(s)
-    monkeypatch.delenv("DRT_AA_TWO_PASS_MIN_SAMPLES")
-    assert renderer.plan(renderer.frame_params(seed=3))["passes"] == 1
-    one = renderer.render(seed=3)
-    monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_SAMPLES", "65536")
-    assert renderer.plan(renderer.frame_params(seed=3))["passes"] == 2
-    two = renderer.render(seed=3)
-    monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_SAMPLES", "65537")
-    assert renderer.plan(renderer.frame_params(seed=3))["passes"] == 1
-    np.testing.assert_array_equal(bits(one), bits(two))
+    monkeypatch.delenv("DRT_AA_TWO_PASS_MIN_MS")
+    r = drt.Renderer(0)
+    try:
+        r.upload(s)
+        assert r.plan(r.frame_params(seed=3))["passes"] == 2  # no completed frame yet
+        two = r.render(seed=3)  # a 64 x 64 x 16 frame takes well under 6 ms
+        assert r.plan(r.frame_params(seed=3))["passes"] == 1
+        one = r.render(seed=3)
+        monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_MS", "0")
+        assert r.plan(r.frame_params(seed=3))["passes"] == 2
+        np.testing.assert_array_equal(bits(one), bits(two))
+    finally:
+        r.close()
 
 
 @pytest.mark.parametrize("accel,spp,kw", [("bvh", 16, {"roughness": 0.1, "max_depth": 8}), ("grid", 9, {"roughness": 0.2}),
