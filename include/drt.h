@@ -210,9 +210,11 @@ typedef struct {
   int32_t mode;
   int32_t persistent;
   int32_t tiles_in_shard;
-  int32_t passes;      /* 2: an in-order frame of a scene without refraction, as a pass over the
-                          pixels' closest-hit chains (samples in order) and a pass over every sample
-                          on its own; 1 otherwise */
+  int32_t passes;      /* 2: a frame of a scene without refraction as a pass over the closest-hit
+                          chains (in-order frames: a pixel's samples in order; AA frames of BVH / Grid
+                          scenes of >= 1024 objects, while the context's newest completed frame took
+                          >= 6 ms or none has completed) and a pass over every sample with its closest
+                          hits read back; 1 otherwise.  Both plans render the same frame. */
   int32_t reserved[4];
 } drt_frame_plan;
 int drt_plan_frame(const drt_ctx* ctx, const drt_frame_params* params, drt_frame_plan* out);
