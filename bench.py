@@ -208,6 +208,22 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
+    # f1 leg: the same scene as a P3F file, written by a child process while the GPU works (np.savetxt
+    # of 3M vertices takes ~10 s of one core), parsed and built after the timed region
+    p3f_writer, p3f_path = None, None
+    # Started before anything touches the GPU, and not under a profiler (rocprofv3 preloads its
+    # library into every child, and with --pmc that library would initialise the GPU in the writer).
+    profiled = "rocprof" in os.environ.get("LD_PRELOAD", "")
+    if rank == 0 and args.scene == "synthetic" and not args.no_load_timing and not profiled:
+        import subprocess
+        import tempfile
+
+        p3f_path = Path(tempfile.gettempdir()) / f"drt_bench_{os.getpid()}_{args.tris}.p3f"
+        code = ("import sys; sys.path.insert(0, %r); from tests import scenegen as sg; "
+                "sg.write_synthetic_p3f(%r, %d, res=(%d, %d), spp=%d, accel=%r, seed=%d, aperture=%r, focal=%r)"
+                % (str(ROOT), str(p3f_path), args.tris, args.res, args.res, args.spp, args.accel, args.seed,
+                   args.aperture, args.focal))
+        p3f_writer = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.DEVNULL)
     import torch
     import torch.distributed as dist
 
@@ -232,19 +248,6 @@ def main():
         if rank == 0:
             print(*a, file=sys.stderr, flush=True)
 
-    # f1 leg: the same scene as a P3F file, written by a child process while the GPU works (np.savetxt
-    # of 3M vertices takes ~10 s of one core), parsed and built after the timed region
-    p3f_writer, p3f_path = None, None
-    if rank == 0 and args.scene == "synthetic" and not args.no_load_timing:
-        import subprocess
-        import tempfile
-
-        p3f_path = Path(tempfile.gettempdir()) / f"drt_bench_{os.getpid()}_{args.tris}.p3f"
-        code = ("import sys; sys.path.insert(0, %r); from tests import scenegen as sg; "
-                "sg.write_synthetic_p3f(%r, %d, res=(%d, %d), spp=%d, accel=%r, seed=%d, aperture=%r, focal=%r)"
-                % (str(ROOT), str(p3f_path), args.tris, args.res, args.res, args.spp, args.accel, args.seed,
-                   args.aperture, args.focal))
-        p3f_writer = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.DEVNULL)
     t0 = time.time()
     tris = synthetic_triangles(args.tris, args.seed) if args.scene == "synthetic" else None
     ext = {"aperture": args.aperture, "focal": args.focal, "roughness": args.roughness,
@@ -265,6 +268,8 @@ def main():
     shard_ps = [r.frame_params(seed=args.seed, shard=rank, n_shards=world, slot=j, **fkw) for j in range(pipe)]
     shard_p = shard_ps[0]
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
+    ref_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, reference_order=True, **fkw)
+    passes = r.plan(shard_p)["passes"]
     frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
     # frames in flight: frame i runs on stream / scratch slot / output buffers i % pipe, so the next
     # frame's kernel fills the CUs the previous frame's tail leaves idle
@@ -298,6 +303,13 @@ def main():
             "cycles_refill", "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
             "wave_leaf_iters", "cycles_leaf", "wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims",
             "wide_verify"]
+    # untimed reference-order stats frame (every shadow query on the reference's binary tree, one
+    # pass): §8(d)'s algorithmic bytes on the reference tree, the basis of rounds 1-3's roofline
+    step(ref_p)
+    torch.cuda.synchronize()
+    st_ref = r.stats()
+    bytes_ref_tree = NODE_BYTES * (st_ref["closest_inner"] + st_ref["shadow_inner"]) + \
+        PRIM_BYTES * (st_ref["closest_prims"] + st_ref["shadow_prims"])
     mine = torch.tensor([st[k] for k in keys], dtype=torch.float64, device="cuda")
     tot = mine.clone()
     if world > 1:
@@ -352,6 +364,10 @@ def main():
         r.render_device(shard_p, (frames[0] if world == 1 else fgs[0].shard).data_ptr(), sptr)
     torch.cuda.synchronize()
     path_ms, total_ms = r.frame_times(serial)
+    try:
+        pass1_ms, pass2_ms = r.frame_pass_times(serial)
+    except AttributeError:  # an A/B build (DRT_LIBRARY) older than drt_frame_pass_times
+        pass1_ms, pass2_ms = [], []
     frame_check = None
     if args.check_frame:
         step(shard_p)  # assemble one more frame, then compare it with a one-shot whole frame
@@ -387,12 +403,14 @@ def main():
     tj = Path(args.traffic_json)
     pmc = {}
     read_bytes = None
+    tr_rec = None
     if world == 1 and tj.exists():
         try:
             # tools/pmc_traffic.py records one entry per workload key: fabric bytes per launch and the
             # pipe ratios (VALU busy against the gfx950 issue peak: a wave64 VALU instruction occupies
             # a SIMD for 2 cycles; kernel cycles = GRBM_GUI_ACTIVE / 8, the counter sums the 8 XCDs)
             tr = json.loads(tj.read_text()).get("workloads", {}).get(workload_key)
+            tr_rec = tr
             if tr:
                 traffic = tr.get("hbm_bytes_per_launch")
                 valu_busy = tr.get("valu_busy")
@@ -416,6 +434,34 @@ def main():
         model = {"t_ms": round(t_hit + t_miss, 3), "t_l2_resident_ms": round(t_hit, 3),
                  "t_fabric_ms": round(t_miss, 3), "missed_records": int(miss),
                  "frac": round((t_hit + t_miss) / kernel_ms, 4)}
+    # Per pass (a two-pass frame: the closest-chain launch, then the replay launch): device time of
+    # each launch in the frames rendered alone after the timed region, its executed algorithmic bytes
+    # (pass 1 traverses the closest-hit queries, pass 2 the shadow queries), its fabric reads from
+    # the PMC record's per-launch entries, and its place against the same ceilings.
+    pass_rows = None
+    if passes == 2 and len(pass1_ms):
+        b1 = NODE_BYTES * mine["closest_inner"] + PRIM_BYTES * mine["closest_prims"]
+        b2 = bytes_launch - b1
+        pmc_passes = (tr_rec or {}).get("passes") or [None, None]
+        pass_rows = []
+        for name, ms, b, pp in (("closest_chain", float(np.mean(pass1_ms)), b1, pmc_passes[0]),
+                                ("replay", float(np.mean(pass2_ms)), b2, pmc_passes[1])):
+            row = {"pass": name, "ms": round(ms, 3), "bytes": int(b), "achieved": round(b / (ms * 1e-3) / 1e9, 1)}
+            if ceiling:
+                row["frac"] = round(row["achieved"] / ceiling["peak_GB_per_s"], 4)
+            if pp and pp.get("read_bytes") is not None:
+                row["fabric_read_bytes"] = pp["read_bytes"]
+                row["write_bytes"] = pp.get("write_size_bytes")
+                if ceiling and ceiling.get("fabric_line_GB_per_s"):
+                    miss = pp["read_bytes"] / 128.0
+                    th = max(0.0, b - 64.0 * miss) / (ceiling["peak_GB_per_s"] * 1e9) * 1e3
+                    tm = 64.0 * miss / (ceiling["fabric_line_GB_per_s"] / 2.0 * 1e9) * 1e3
+                    row["two_level_model_ms"] = round(th + tm, 3)
+                    row["two_level_frac"] = round((th + tm) / ms, 4)
+                for k in ("valu_busy", "tcc_hit_rate"):
+                    if pp.get(k) is not None:
+                        row[k] = round(pp[k], 4)
+            pass_rows.append(row)
     value = rays_frame * args.steps / dt / 1e6
     out = {
         "metric": "Mrays/s + frame ms at 512x512x64spp, 1M-tri BVH scene, 1/2/4/8 MI355X",
@@ -459,6 +505,14 @@ def main():
                      "two_level_model": model,
                      "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),
+                     # §8(d)'s bytes (64 B per inner visit + 48 B per primitive test) on the reference's
+                     # binary tree for every query (a DRT_FRAME_REFERENCE_ORDER stats frame): the basis
+                     # rounds 1-3 quoted, over the same kernel time
+                     "bytes_ref_tree": int(bytes_ref_tree),
+                     "frac_ref_tree": round(bytes_ref_tree / (kernel_ms * 1e-3) / 1e9 / ceiling["peak_GB_per_s"], 4)
+                     if ceiling else None,
+                     "passes": pass_rows,
+                     "pass_sum_ms": round(float(np.mean(pass1_ms) + np.mean(pass2_ms)), 3) if len(pass1_ms) else None,
                      "ceiling": ceiling},
         "host_output_frame_ms": None if host_frame_ms is None else round(host_frame_ms, 3),
         **({"frame_check_vs_whole_frame": frame_check} if args.check_frame else {}),

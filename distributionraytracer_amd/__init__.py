@@ -338,6 +338,16 @@ class Renderer:
             check(n, self.h, "drt_frame_times")
         return np.array(a[:n]), np.array(b[:n])
 
+    def frame_pass_times(self, max_frames=512):
+        """(pass-1 ms, pass-2 ms) per recent frame, oldest first (HIP events): a two-pass frame's
+        closest-chain and replay launches; a one-pass frame's kernel and 0."""
+        a = (C.c_double * max_frames)()
+        b = (C.c_double * max_frames)()
+        n = _lib.load().drt_frame_pass_times(self.h, max_frames, a, b)
+        if n < 0:
+            check(n, self.h, "drt_frame_pass_times")
+        return np.array(a[:n]), np.array(b[:n])
+
     def frame_spans(self, max_frames=512):
         """(path start, path end, frame end) of recent frames in ms on one device clock, from the
         oldest frame's path-kernel start (HIP events on each frame's stream)."""

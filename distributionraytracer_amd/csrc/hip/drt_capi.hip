@@ -62,6 +62,7 @@ struct drt_ctx {
   // per-frame HIP events (path-kernel start, path-kernel end / reduce start, frame end),
   // a ring so every frame of a timed loop can be read back afterwards
   static constexpr int kRing = 512;
+  static constexpr int kEv = 4;  // events per frame: start, path end, frame end, end of pass 1
   std::vector<hipEvent_t> ring;
   uint64_t frames = 0;
   std::string err;
@@ -95,6 +96,7 @@ struct drt_ctx {
   float gmin[3] = {0}, gmax[3] = {0};
   DevBuf d_cell_start, d_cell_objs, d_macro, d_cell_recs;
   DevBuf d_gprims, d_cell_pos;  // indexed Grid layout (experiment): Morton-ordered records, per-reference positions
+  DevBuf d_cell_tris, d_cell_tpos;  // triangle scenes: 40-B triangles in pairs per cell, pair-aligned cell starts
   int gmacro_shift = 0, gmacro_dim[3] = {0, 0, 0}, gmacro_words = 0;
   // frame scratch
   DevBuf d_frame, d_rays, d_out, d_counter;
@@ -163,9 +165,9 @@ static int env_int(const char* name, int dflt) {  // tuning knobs for A/B runs
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }
-static double env_double(const char* name, double dflt) {
+static uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* v = getenv(name);
-  return v && *v ? atof(v) : dflt;
+  return (v && *v) ? strtoull(v, nullptr, 0) : dflt;
 }
 
 static PrimRecord pack_prim(const drt_prim& p, uint32_t mat, uint32_t obj) {
@@ -203,6 +205,8 @@ static bool quantize_axis(const double* lo, const double* hi, int n, float& p, u
     nhi = std::max(nhi, hi[k]);
   }
   if (!std::isfinite(nlo) || !std::isfinite(nhi) || nhi < nlo) return false;
+  // the device's one-fma child test assumes |anchor| <= 2^60 and scale <= 2^50 (node_step)
+  if (std::fabs(nlo) > 0x1p59 || std::fabs(nhi) > 0x1p59) return false;
   int e0 = -126;
   if (nhi > nlo) e0 = std::max(-126, std::ilogb((nhi - nlo) / 255.0) - 1);
   for (int E = e0; E <= 120; E++) {
@@ -213,6 +217,7 @@ static bool quantize_axis(const double* lo, const double* hi, int n, float& p, u
     bool ok = true;
     const float pf = (float)(k0 * s), sf = (float)s;
     if ((double)pf != k0 * s) continue;
+    if (E > 50) return false;
     for (int k = 0; k < 4 && ok; k++) {
       if (k >= n) {  // unused slot: an inverted box (lo 255 > hi 0)
         L |= 255u << (8 * k);
@@ -240,6 +245,39 @@ static bool quantize_axis(const double* lo, const double* hi, int n, float& p, u
     return true;
   }
   return false;
+}
+
+// The shadow tree answers exactly as the reference's tree only if every child box lies inside its
+// parent's box and every primitive sits in exactly one leaf.  The reference's build
+// guarantees both (bvh.cpp:206-220: a node's box is the union of its objects' boxes); a caller's
+// tree that breaks either — or shares a subtree between two parents, which the collapse would copy
+// once per parent — keeps the binary tree for its shadow queries.
+static bool wide_tree_valid(const drt_bvh_node* nodes, uint32_t n_nodes, uint32_t n_obj) {
+  std::vector<uint8_t> seen(n_nodes, 0), covered(n_obj, 0);
+  std::vector<uint32_t> st{0u};
+  seen[0] = 1;
+  uint64_t leaf_objs = 0;
+  while (!st.empty()) {
+    const uint32_t i = st.back();
+    st.pop_back();
+    const drt_bvh_node& nd = nodes[i];
+    if (nd.leaf) {
+      for (uint32_t k = 0; k < nd.n_objs; k++) {
+        if (covered[nd.index + k]) return false;
+        covered[nd.index + k] = 1;
+      }
+      leaf_objs += nd.n_objs;
+      continue;
+    }
+    for (uint32_t c = nd.index; c < nd.index + 2; c++) {
+      if (seen[c]) return false;
+      seen[c] = 1;
+      for (int a = 0; a < 3; a++)
+        if (!(nodes[c].bmin[a] >= nd.bmin[a]) || !(nodes[c].bmax[a] <= nd.bmax[a])) return false;
+      st.push_back(c);
+    }
+  }
+  return leaf_objs == n_obj;
 }
 
 // Collapse the reference's binary tree (nodes, leaf descriptors per node) into 4-ary records: a
@@ -341,7 +379,7 @@ int drt_create(drt_ctx** out, const drt_options* opt) {
     delete c;
     return DRT_E_HIP;
   }
-  c->ring.assign(3 * drt_ctx::kRing, nullptr);
+  c->ring.assign(drt_ctx::kEv * drt_ctx::kRing, nullptr);
   for (auto& e : c->ring)
     if (hipEventCreate(&e) != hipSuccess) {
       drt_destroy(c);
@@ -589,7 +627,8 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
   // 4-ary shadow tree and the exact reference leaf box of every primitive (DRT_WIDE_SHADOW=0: none)
   std::vector<WideNodeRecord> wide;
   uint32_t wroot = 0;
-  const bool has_wide = env_int("DRT_WIDE_SHADOW", 1) != 0 && build_wide(nodes, dsc, wide, wroot);
+  const bool has_wide = env_int("DRT_WIDE_SHADOW", 1) != 0 && wide_tree_valid(nodes, n_nodes, n_obj) &&
+                        build_wide(nodes, dsc, wide, wroot);
   std::vector<LeafBoxRecord> lbox;
   if (has_wide) {
     lbox.assign((size_t)n_obj + 2, LeafBoxRecord{});  // + 2: the node step's tail slot reads
@@ -676,9 +715,48 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   DRT_HIP(c, hipMemcpy(c->d_cell_start.p, s32.data(), 4 * s32.size(), hipMemcpyHostToDevice));
   DRT_HIP(c, c->d_cell_objs.ensure(4 * std::max<size_t>(1, o32.size())));
   if (!o32.empty()) DRT_HIP(c, hipMemcpy(c->d_cell_objs.p, o32.data(), 4 * o32.size(), hipMemcpyHostToDevice));
-  // the persistent Grid stepper reads the referenced records inline, in cell order (48 B per
-  // reference; q2.w = the scene-order primitive index), so a cell's objects are one hop away
-  {
+  // Triangle scenes (round 5): the referenced triangles inline in cell order as 40-B records
+  // (v0, e1, e2, scene index), two per 80-B pair = five 16-B loads instead of six for two 48-B
+  // records (the stepper is bound by the per-lane loads of the vector-memory path), and
+  // 132 instead of 158 MB at 1M triangles.  A cell's list starts on a pair boundary: cell_tpos[i] is
+  // its first record (even), bit 31 set when cell i - 1's list ended on a padding slot, so a cell's
+  // range is [tpos[i], tpos[i + 1] - pad) from one 8-B load.
+  if (c->tri_only) {
+    std::vector<uint32_t> tpos(ncell + 1);
+    uint64_t pos = 0;
+    uint32_t pad = 0;
+    for (size_t i = 0; i < ncell; i++) {
+      const uint32_t cnt = s32[i + 1] - s32[i];
+      tpos[i] = (uint32_t)pos | (pad << 31);
+      pos += cnt + (cnt & 1u);
+      pad = cnt & 1u;
+    }
+    if (pos >= 0x80000000ull) DRT_FAIL(c, DRT_E_UNSUPPORTED, "too many grid references");
+    tpos[ncell] = (uint32_t)pos | (pad << 31);
+    std::vector<float> tris((size_t)(pos / 2 + 1) * 20, 0.0f);
+    for (size_t i = 0; i < ncell; i++)
+      for (uint32_t k = s32[i], j = 0; k < s32[i + 1]; k++, j++) {
+        const uint32_t at = (tpos[i] & 0x7fffffffu) + j;  // record position
+        float* f = &tris[(size_t)(at >> 1) * 20 + (at & 1u) * 10];
+        const PrimRecord& r = c->prims_scene[o32[k]];  // (v0, .), (e1, .), (e2, .)
+        memcpy(f, &r.q[0], 12);
+        memcpy(f + 3, &r.q[4], 12);
+        memcpy(f + 6, &r.q[8], 12);
+        memcpy(f + 9, &o32[k], 4);
+      }
+    DRT_HIP(c, c->d_cell_tpos.ensure(4 * tpos.size()));
+    DRT_HIP(c, hipMemcpy(c->d_cell_tpos.p, tpos.data(), 4 * tpos.size(), hipMemcpyHostToDevice));
+    DRT_HIP(c, c->d_cell_tris.ensure(4 * tris.size() + kPrimPadBytes));
+    DRT_HIP(c, hipMemset(c->d_cell_tris.p, 0, 4 * tris.size() + kPrimPadBytes));
+    DRT_HIP(c, hipMemcpy(c->d_cell_tris.p, tris.data(), 4 * tris.size(), hipMemcpyHostToDevice));
+    c->d_cell_recs.release();
+  } else {
+    c->d_cell_tris.release();
+    c->d_cell_tpos.release();
+  }
+  // other scenes' persistent Grid stepper reads the referenced records inline, in cell order (48 B
+  // per reference; q2.w = the scene-order primitive index), so a cell's objects are one hop away
+  if (!c->tri_only) {
     std::vector<PrimRecord> recs((size_t)std::max<int64_t>(1, n_refs));
     for (int64_t i = 0; i < n_refs; i++) {
       recs[i] = c->prims_scene[o32[i]];
@@ -690,7 +768,9 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   }
   // Indexed layout (experiment, drt_kernels.hip DRT_GRID_INDEXED): every object's record once, in the
   // order a Morton walk of the non-empty cells first meets it (q2.w = the scene-order index), and per
-  // reference its position there — so that objects of neighbouring cells share lines
+  // reference its position there — so that objects of neighbouring cells share lines.  Built and
+  // uploaded only by builds that read it.
+#ifdef DRT_GRID_INDEXED
   {
     auto part = [](uint32_t v) {  // 10 bits -> every third bit
       v &= 0x3ffu;
@@ -729,6 +809,7 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
     DRT_HIP(c, c->d_cell_pos.ensure(4 * pos.size()));
     DRT_HIP(c, hipMemcpy(c->d_cell_pos.p, pos.data(), 4 * pos.size(), hipMemcpyHostToDevice));
   }
+#endif
   // grid references index scene-order primitive records
   DRT_HIP(c, hipMemcpy(c->d_prims.p, c->prims_scene.data(), sizeof(PrimRecord) * c->prims_scene.size(),
                        hipMemcpyHostToDevice));
@@ -801,6 +882,8 @@ static int scene_args(drt_ctx* c, int accel, SceneArgs& S, bool reference_order)
     S.cell_start = c->d_cell_start.as<uint32_t>();
     S.gmacro = c->d_macro.as<uint32_t>();
     S.cell_recs = c->d_cell_recs.as<float4>();
+    S.cell_tris = c->d_cell_tris.as<float4>();
+    S.cell_tpos = c->d_cell_tpos.as<uint32_t>();
     S.gprims = c->d_gprims.as<float4>();
     S.cell_pos = c->d_cell_pos.as<uint32_t>();
     S.gmacro_shift = c->gmacro_shift;
@@ -818,6 +901,7 @@ struct Plan {
   bool persistent;      // path_persistent (BVH) instead of path_kernel
   bool two_pass;        // in-order frame as MODE_SKEL + MODE_REPLAY (no refraction in the scene)
   bool aa_chain;        // ... or an AA frame as MODE_CHAIN + MODE_REPLAY (BVH, shadow tree uploaded)
+  uint32_t chain_div;   // two-pass Whitted frame: replay sample slots per closest-chain record (grid_res)
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -916,21 +1000,45 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // spp: 2.72 / 2.15 ms Grid / BVH in two passes against 2.02 / 1.63 in one; balls_high 512^2 x 16:
   // BVH 5.21 against 4.79 ms), while longer frames gain (the 1M-triangle scene at 512^2 x 16 spp:
   // 22.3 against 24.3 ms; profiles/r04_two_pass_small_frames_ab.txt, r04_two_pass_frame_time_ab.jsonl).
-  // The context's newest completed frame decides, as for the auxiliary streams: two passes while no
-  // frame has completed or the last one's path kernels took >= DRT_AA_TWO_PASS_MIN_MS (default 6 ms).
-  // Both plans render the same frame.
-  note_last_path_ms(c);
-  const bool big_frame = c->last_path_ms < 0.0 || c->last_path_ms >= env_double("DRT_AA_TWO_PASS_MIN_MS", 6.0);
+  // The plan depends on the params and the scene only (round 5; round 4 read the context's last frame
+  // time, so equal frames could plan differently): two passes for whole frames of >= 2^23 samples
+  // (C3, the headline, their shards) or scenes of >= 2^19 objects (the 1M-triangle scene at 16 spp);
+  // the shipped scenes' 16-spp frames (<= 800x600 x 16 = 7.7 M samples, <= 100 005 objects) keep one.
+  // DRT_AA_TWO_PASS: 0 one pass, 1 this rule (default), 2 two passes at any size.  Both plans render
+  // the same frame.
+  const int aa2 = env_int("DRT_AA_TWO_PASS", 1);
+  const uint64_t frame_samples = (uint64_t)P.n_tiles * F.tile * F.tile * (uint64_t)per_pixel;
+  const bool big_frame = aa2 >= 2 || frame_samples >= (env_u64("DRT_AA_TWO_PASS_MIN_SAMPLES", 1ull << 23)) ||
+                         (uint64_t)c->n_prims >= env_u64("DRT_AA_TWO_PASS_BIG_SCENE", 1ull << 19);
   // The Grid's AA frames too (its shadow queries stay on the Grid: Grid::Traverse(Ray&)'s answer is
   // tied to the cells its walk visits): 1 381 against 1 295 Mrays/s on the Grid headline scene.
   const bool grid_chain = c->accel == DRT_ACCEL_GRID && c->has_grid && env_int("DRT_AA_TWO_PASS_GRID", 1) != 0;
   if (P.persistent && F.mode == MODE_AA && big_frame && (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) &&
-      !(p->flags & DRT_FRAME_REFERENCE_ORDER) && env_int("DRT_AA_TWO_PASS", 1) != 0 &&
+      !(p->flags & DRT_FRAME_REFERENCE_ORDER) && aa2 != 0 &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
     bool refr = false;
     for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
     P.two_pass = P.aa_chain = !refr;
+  }
+  // Whitted frames in two passes too (round 5): the closest-chain pass traces ONE chain per pixel —
+  // its grid_res light samples share the pixel-centre primary ray and every mirror bounce
+  // (main.cpp:683-696; roughness 0, or the frame is MODE_SEQ) — and the replay pass runs every
+  // (pixel, light sample) with that pixel's hits read back, its shadow queries on the shadow tree
+  // (BVH) or the Grid.  Same conditions as the AA frames'; a quad-light frame of >= 4 light samples
+  // at any size (the closest work shrinks grid_res times), a point-light frame by the AA size rule.
+  // DRT_WHITTED_TWO_PASS=0 keeps one pass.
+  P.chain_div = 1;
+  const bool whitted = F.mode == MODE_WHITTED_QUAD || F.mode == MODE_WHITTED_POINT;
+  if (P.persistent && whitted && env_int("DRT_WHITTED_TWO_PASS", 1) != 0 && aa2 != 0 &&
+      (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
+      (F.mode == MODE_WHITTED_QUAD ? F.grid_res >= 4 || aa2 >= 2 : big_frame) &&
+      c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) && !(p->flags & DRT_FRAME_REFERENCE_ORDER) &&
+      P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
+    bool refr = false;
+    for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
+    P.two_pass = P.aa_chain = !refr;
+    P.chain_div = F.mode == MODE_WHITTED_QUAD ? (uint32_t)F.nsub : 1u;
   }
   ReduceArgs& R = P.R;
   R.nsub = slots;
@@ -945,7 +1053,7 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
 static void note_last_path_ms(drt_ctx* c) {
   const uint64_t look = std::min<uint64_t>(c->frames, 4);
   for (uint64_t k = 0; k < look; k++) {
-    hipEvent_t* ev = &c->ring[3 * ((c->frames - 1 - k) % drt_ctx::kRing)];
+    hipEvent_t* ev = &c->ring[drt_ctx::kEv * ((c->frames - 1 - k) % drt_ctx::kRing)];
     if (hipEventQuery(ev[1]) != hipSuccess) continue;
     float ms = 0.0f;
     if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) c->last_path_ms = ms;
@@ -971,12 +1079,13 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // The slot's scratch is reused: a frame from another stream than the slot's last frame waits for
   // that frame to end (on the device).  Frames of one stream are ordered by the stream itself.
   if (c->slot_used[slot] && c->slot_stream[slot] != st && c->frames - c->slot_frame[slot] < drt_ctx::kRing)
-    DRT_HIP(c, hipStreamWaitEvent(st, c->ring[3 * (c->slot_frame[slot] % drt_ctx::kRing) + 2], 0));
+    DRT_HIP(c, hipStreamWaitEvent(st, c->ring[drt_ctx::kEv * (c->slot_frame[slot] % drt_ctx::kRing) + 2], 0));
   // Two-pass in-order frame: its closest-hit record is allocated first; a frame whose record does not
   // fit in device memory runs as the one-pass MODE_SEQ frame, which renders the same pixels.
   if (P.F.n_items && P.two_pass) {
     if ((!P.aa_chain && c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess) ||
-        c->d_skel_hits_s[slot].ensure(sizeof(uint2) * P.n_slots * (uint64_t)(P.F.max_depth + 1)) != hipSuccess) {
+        c->d_skel_hits_s[slot].ensure(sizeof(uint2) * (P.n_slots / P.chain_div) * (uint64_t)(P.F.max_depth + 1)) !=
+            hipSuccess) {
       (void)hipGetLastError();
       c->d_skel_rk_s[slot].release();
       c->d_skel_hits_s[slot].release();
@@ -998,7 +1107,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       for (int k = 0; k < DRT_FRAME_SLOTS && !handover; k++) {
         if (k == slot || !c->slot_used[k] || c->slot_stream[k] == st) continue;
         if (c->frames - c->slot_frame[k] >= drt_ctx::kRing) continue;
-        handover = hipEventQuery(c->ring[3 * (c->slot_frame[k] % drt_ctx::kRing) + 2]) == hipErrorNotReady;
+        handover = hipEventQuery(c->ring[drt_ctx::kEv * (c->slot_frame[k] % drt_ctx::kRing) + 2]) == hipErrorNotReady;
       }
     }
   }
@@ -1034,7 +1143,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       DRT_HIP(c, hipStreamWaitEvent(st, c->ev_shuf[slot], 0));
     }
   }
-  hipEvent_t* ev = &c->ring[3 * (c->frames % drt_ctx::kRing)];
+  hipEvent_t* ev = &c->ring[drt_ctx::kEv * (c->frames % drt_ctx::kRing)];
   c->slot_frame[slot] = c->frames;
   c->slot_stream[slot] = st;
   c->slot_used[slot] = true;
@@ -1081,6 +1190,12 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F1.skel_rk = P.aa_chain ? nullptr : d_rk.as<uint32_t>();
     F1.skel_hits = d_hits.as<uint2>();
     F1.aa_chain = P.aa_chain ? 1 : 0;
+    F1.chain_div = (int)P.chain_div;
+    if (P.chain_div > 1) {  // a Whitted frame's closest-chain pass: one lane per pixel
+      F1.nsub = 1;
+      F1.n_items = P.F.n_items / P.chain_div;
+      F1.part_items = (uint32_t)((F1.n_items + 7) / 8);
+    }
     if (P.aa_chain) {  // the closest-chain pass carries little state
       // its "shading" is recording a hit and starting the mirror ray: batches of 8 ready lanes
       // measured 1 927 against 1 897 Mrays/s for 24 (1: 1 842, 48: 1 725; profiles/r04_pass_knobs_ab.jsonl)
@@ -1099,8 +1214,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F1.seq_cont = nullptr;
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());
+    DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
     F2.mode = MODE_REPLAY;
+    F2.nsub = P.F.nsub;
     F2.waves = env_int("DRT_REPLAY_WAVES", P.F.waves);
     F2.process_min = env_int("DRT_REPLAY_PROCESS_MIN", P.F.process_min);  // 12 / 40: 1 861 / 1 764 vs 1 897
     F2.refill_min = env_int("DRT_REPLAY_REFILL_MIN", P.F.refill_min);
@@ -1115,6 +1232,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     else launch_path(S, P.F, c->accel, c->tri_only, stats, st);
   }
   DRT_HIP(c, hipGetLastError());
+  if (!(P.F.n_items && P.two_pass)) DRT_HIP(c, hipEventRecord(ev[3], st));  // one pass: pass 1 is the frame
   DRT_HIP(c, hipEventRecord(ev[1], st));
   DRT_HIP(c, hipEventRecord(c->ev_path[slot], st));  // every frame: the slot's last path kernel
   c->path_issued[slot] = true;
@@ -1211,13 +1329,31 @@ int drt_frame_times(drt_ctx* c, int max_frames, double* path_ms, double* total_m
   const int n = (int)std::min<uint64_t>(have, (uint64_t)max_frames);
   for (int i = 0; i < n; i++) {
     const uint64_t f = c->frames - (uint64_t)n + (uint64_t)i;
-    hipEvent_t* ev = &c->ring[3 * (f % drt_ctx::kRing)];
+    hipEvent_t* ev = &c->ring[drt_ctx::kEv * (f % drt_ctx::kRing)];
     DRT_HIP(c, hipEventSynchronize(ev[2]));
     float a = 0, b = 0;
     DRT_HIP(c, hipEventElapsedTime(&a, ev[0], ev[1]));
     DRT_HIP(c, hipEventElapsedTime(&b, ev[0], ev[2]));
     if (path_ms) path_ms[i] = a;
     if (total_ms) total_ms[i] = b;
+  }
+  return n;
+}
+
+int drt_frame_pass_times(drt_ctx* c, int max_frames, double* pass1_ms, double* pass2_ms) {
+  if (!c || max_frames < 0) return DRT_E_INVALID;
+  const uint64_t have = std::min<uint64_t>(c->frames, (uint64_t)drt_ctx::kRing);
+  const int n = (int)std::min<uint64_t>(have, (uint64_t)max_frames);
+  if (n) DRT_HIP(c, hipSetDevice(c->device));
+  for (int i = 0; i < n; i++) {
+    const uint64_t f = c->frames - (uint64_t)n + (uint64_t)i;
+    hipEvent_t* ev = &c->ring[drt_ctx::kEv * (f % drt_ctx::kRing)];
+    DRT_HIP(c, hipEventSynchronize(ev[2]));
+    float a = 0, b = 0;
+    DRT_HIP(c, hipEventElapsedTime(&a, ev[0], ev[3]));
+    DRT_HIP(c, hipEventElapsedTime(&b, ev[3], ev[1]));
+    if (pass1_ms) pass1_ms[i] = a;
+    if (pass2_ms) pass2_ms[i] = b;
   }
   return n;
 }
@@ -1229,9 +1365,9 @@ int drt_frame_spans(drt_ctx* c, int max_frames, double* path_start, double* path
   if (n == 0) return 0;
   DRT_HIP(c, hipSetDevice(c->device));
   const uint64_t f0 = c->frames - (uint64_t)n;
-  hipEvent_t base = c->ring[3 * (f0 % drt_ctx::kRing)];
+  hipEvent_t base = c->ring[drt_ctx::kEv * (f0 % drt_ctx::kRing)];
   for (int i = 0; i < n; i++) {
-    hipEvent_t* ev = &c->ring[3 * ((f0 + (uint64_t)i) % drt_ctx::kRing)];
+    hipEvent_t* ev = &c->ring[drt_ctx::kEv * ((f0 + (uint64_t)i) % drt_ctx::kRing)];
     DRT_HIP(c, hipEventSynchronize(ev[2]));
     float a = 0, b = 0, e = 0;
     DRT_HIP(c, hipEventElapsedTime(&a, base, ev[0]));
@@ -1248,7 +1384,7 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
   if (!c || !out) return DRT_E_INVALID;
   memset(&c->last, 0, sizeof(c->last));
   if (c->frames > 0) {
-    hipEvent_t* ev = &c->ring[3 * ((c->frames - 1) % drt_ctx::kRing)];
+    hipEvent_t* ev = &c->ring[drt_ctx::kEv * ((c->frames - 1) % drt_ctx::kRing)];
     DRT_HIP(c, hipSetDevice(c->device));
     DRT_HIP(c, hipEventSynchronize(ev[2]));
     float ms_k = 0, ms_all = 0;

@@ -819,6 +819,17 @@ __device__ __forceinline__ bool ray_finite(const RayP& r) {
   return inv_finite(r) && fabsf(r.o.x) < __builtin_inff() && fabsf(r.o.y) < __builtin_inff() &&
          fabsf(r.o.z) < __builtin_inff();
 }
+// Shadow-tree lanes (the one-fma child test's range, node_step): |inv| <= 2^40 (no direction
+// component below ~1e-12 of the ray's length) and |o| <= 2^60.  Other rays walk the binary tree.
+__device__ __forceinline__ bool wide_ray_ok(const RayP& r) {
+#ifdef DRT_WIDE_EXACT
+  return ray_finite(r);
+#else
+  const float mi = fmaxf(fmaxf(fabsf(r.ix), fabsf(r.iy)), fabsf(r.iz));
+  const float mo = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
+  return mi <= 0x1p40f && mo <= 0x1p60f;  // false for NaN
+#endif
+}
 
 // Grid::Init_Traverse (grid.cpp:160-245) for the lane's query: grid-box entry, first cell and
 // the double-precision DDA state, exactly as grid_traverse computes them.  False: box missed.
@@ -930,7 +941,11 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   uint32_t b = 0, e = 0;  // LF_EMPTY: the cell lies in an empty macro-cell (the last call's walk)
   if (!(fl & LF_EMPTY)) {  // the cell's range [start, next start) in one 8-B load (4-B aligned)
     uint2 r;
-    __builtin_memcpy(&r, S.cell_start + cidx, sizeof(r));
+    __builtin_memcpy(&r, (TRI_ONLY ? S.cell_tpos : S.cell_start) + cidx, sizeof(r));
+    if (TRI_ONLY) {  // pair-aligned starts; bit 31 of the next start: this list ends on a padding slot
+      r.x &= 0x7fffffffu;
+      r.y = (r.y & 0x7fffffffu) - (r.y >> 31);
+    }
     b = resume ? L.spa : r.x;
     e = r.y;
   }
@@ -985,13 +1000,31 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
       c2 = r2[2];
     }
 #else
-    const float4* r = S.cell_recs + 3 * (size_t)q;
-    const float4 a0 = r[0], a1 = r[1], a2 = r[2];
-    float4 c0, c1, c2;
-    if (two) {
-      c0 = r[3];
-      c1 = r[4];
-      c2 = r[5];
+    float4 a0, a1, a2, c0, c1, c2;
+    if (TRI_ONLY) {  // a pair of 40-B triangle records (q is even): five 16-B loads, three for one
+      const float4* r = S.cell_tris + 5 * (size_t)(q >> 1);
+      const float4 x0 = r[0], x1 = r[1], x2 = r[2];
+      float4 x3, x4;
+      if (two) {
+        x3 = r[3];
+        x4 = r[4];
+      }
+      a0 = make_float4(x0.x, x0.y, x0.z, 0.0f);      // v0
+      a1 = make_float4(x0.w, x1.x, x1.y, 0.0f);      // e1
+      a2 = make_float4(x1.z, x1.w, x2.x, x2.y);      // e2, scene index
+      c0 = make_float4(x2.z, x2.w, x3.x, 0.0f);
+      c1 = make_float4(x3.y, x3.z, x3.w, 0.0f);
+      c2 = make_float4(x4.x, x4.y, x4.z, x4.w);
+    } else {
+      const float4* r = S.cell_recs + 3 * (size_t)q;
+      a0 = r[0];
+      a1 = r[1];
+      a2 = r[2];
+      if (two) {
+        c0 = r[3];
+        c1 = r[4];
+        c2 = r[5];
+      }
     }
 #endif
     test(a0, a1, a2);
@@ -1073,7 +1106,7 @@ __device__ __forceinline__ void start_query(const SceneArgs& S, Lane& L, const R
   L.fl = (L.fl & LF_OUTSIDE) | (shadow ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (fin ? LF_FINITE : 0u);
   // finite shadow rays walk the 4-ary shadow tree; the others keep the reference's slab NaN rules
   // on its binary tree
-  if (WIDE && shadow && fin && S.wnodes != nullptr) {
+  if (WIDE && shadow && fin && S.wnodes != nullptr && wide_ray_ok(q)) {
     if (STATS) C.v[ST_W_RAYS]++;
     L.fl |= LF_WIDE;
     L.cur = S.wroot;
@@ -1201,7 +1234,38 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
         tn[2 * h + j] = t0;
       }
     }
-#else
+#elif !defined(DRT_WIDE_EXACT)
+    // Round 5: each plane as ONE fma, t = q * S + B with B = (p - o) * inv and S = 2^E * inv per axis
+    // and node, instead of (fma(q, 2^E, p) - o) * inv (two more VALU per plane, 48 per node).  The
+    // value is not the reference arithmetic's on the decoded plane, so the test is widened by a
+    // bound on the difference: with M = max over axes of |B| + 255 |S| >= every |t| of
+    // the node, both computations are within 5.0003 eps M of the exact real (P - o) * inv (eps =
+    // 2^-24: B rounds twice, the fma once; the reference arithmetic twice), so testing
+    // max(t0, 0) < t1 + 2D with 2D = 2^-20 M (+ 2^-99 for results near underflow, where |S| may have
+    // lost bits) accepts every child the reference arithmetic accepts on the decoded box, hence
+    // every child whose reference box the ray hits.  The extra children it may accept are ones the
+    // exact decode rejected by < 1e-6 of their distance; the leaf-box check (LF_VERIFY) keeps the
+    // answer exact.  Only lanes with |inv| <= 2^40 and |o| <= 2^60 walk the shadow tree
+    // (wide_ray_ok), and build_wide keeps |p| <= 2^60 and 2^E <= 2^50, so nothing here overflows.
+    const float Bx = (s0.x - L.q.o.x) * L.q.ix, By = (s0.y - L.q.o.y) * L.q.iy, Bz = (s0.z - L.q.o.z) * L.q.iz;
+    const float Sx = scx * L.q.ix, Sy = scy * L.q.iy, Sz = scz * L.q.iz;
+    const float M = fmaxf(fmaxf(__builtin_fmaf(255.0f, fabsf(Sx), fabsf(Bx)), __builtin_fmaf(255.0f, fabsf(Sy), fabsf(By))),
+                          __builtin_fmaf(255.0f, fabsf(Sz), fabsf(Bz)));
+    const float D2 = __builtin_fmaf(M, 0x1p-20f, 0x1p-99f);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int sh = 8 * k;
+      const float tnx = __builtin_fmaf((float)((nx >> sh) & 0xffu), Sx, Bx);
+      const float tfx = __builtin_fmaf((float)((fx >> sh) & 0xffu), Sx, Bx);
+      const float tny = __builtin_fmaf((float)((ny >> sh) & 0xffu), Sy, By);
+      const float tfy = __builtin_fmaf((float)((fy >> sh) & 0xffu), Sy, By);
+      const float tnz = __builtin_fmaf((float)((nz >> sh) & 0xffu), Sz, Bz);
+      const float tfz = __builtin_fmaf((float)((fz >> sh) & 0xffu), Sz, Bz);
+      const float t0 = fmaxf(fmaxf(tnx, tny), tnz), t1 = fminf(fminf(tfx, tfy), tfz);
+      hk[k] = fmaxf(t0, 0.0f) < t1 + D2;
+      tn[k] = t0;
+    }
+#else  // DRT_WIDE_EXACT (A/B): the reference arithmetic on the decoded planes
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int sh = 8 * k;
@@ -1446,7 +1510,9 @@ template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void closest_query(const SceneArgs& S, const FrameArgs& F, Lane& L, const RayP& q,
                                               Counters& C) {
   if (MODE == MODE_REPLAY) {
-    const uint2 h = F.skel_hits[(size_t)L.item * (uint32_t)(F.max_depth + 1) + (uint32_t)(L.depth - 1)];
+    // a Whitted frame's light samples share their pixel's record (FrameArgs::chain_div)
+    const uint32_t rec = F.chain_div > 1 ? L.item / (uint32_t)F.chain_div : L.item;
+    const uint2 h = F.skel_hits[(size_t)rec * (uint32_t)(F.max_depth + 1) + (uint32_t)(L.depth - 1)];
     L.q = q;
     L.best_t = __uint_as_float(h.x);
     L.best_prim = h.y;
@@ -1858,9 +1924,9 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
   L.fsp = 0;
   L.ior1 = 1.0f;
   L.fl = 0u;
-  if (STATS) C.v[ST_SAMPLES]++;
+  if (STATS) C.v[ST_SAMPLES] += MODE == MODE_CHAIN ? (uint32_t)F.chain_div : 1u;
   RayP r;
-  if (MODE == MODE_AA || MODE == MODE_CHAIN) {
+  if (MODE == MODE_AA || (MODE == MODE_CHAIN && F.spp > 0)) {
     const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     float rx, ry, sx, sy;
     const int pos = F.perm ? (int)F.perm[item] : shuffle_source(F, pmix, it.sub);  // item = pixel * spp + sub
@@ -1872,7 +1938,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     L.ls = mk(((float)(s % F.grid_size) + 0.5f) / (float)F.grid_size,
               ((float)(s / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f);
     r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
-  } else {
+  } else {  // MODE_WHITTED_POINT, and a Whitted frame's closest-chain pass (one lane per pixel)
     L.ls = mk(0.5f, 0.5f, 0.0f);
     r = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
   }
@@ -2162,7 +2228,7 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
           const bool fin = ray_finite(L.q);
           L.fl = (KIND == 2 ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (fin ? LF_FINITE : 0u);
           if (STATS) C.v[KIND == 2 ? ST_SHADOW : ST_CLOSEST]++;
-          if (KIND == 2 && fin && S.wnodes != nullptr) {  // finite shadow rays: the 4-ary shadow tree
+          if (KIND == 2 && fin && S.wnodes != nullptr && wide_ray_ok(L.q)) {  // finite shadow rays: the 4-ary shadow tree
             if (STATS) C.v[ST_W_RAYS]++;
             L.fl |= LF_WIDE;
             L.cur = S.wroot;

@@ -25,7 +25,8 @@ enum FrameMode : int {
   // An AA frame (MODE_AA) of a refraction-free BVH scene in two passes (round 4), so that the
   // shadow queries run in waves of shadow queries only, on the 4-ary shadow tree:
   MODE_CHAIN = 7    // pass 1, one lane per (pixel, sample): the sample's closest-hit chain only,
-                    // each bounce's hit recorded; pass 2 is MODE_REPLAY
+                    // each bounce's hit recorded; pass 2 is MODE_REPLAY.  A Whitted frame (spp 0,
+                    // round 5) in two passes: one lane per pixel, the chain its light samples share
 };
 
 enum StatSlot : int {
@@ -100,6 +101,10 @@ struct SceneArgs {
   // cell of that macro-cell holds an object
   const uint32_t* gmacro;
   const float4* cell_recs;  // per reference, in cell order: the primitive record, q2.w = its index
+  // triangle scenes: per reference in cell order a 40-B (v0, e1, e2, scene index) record, two per
+  // 80-B pair; cell i's records [tpos[i] & 0x7fffffff, (tpos[i+1] & 0x7fffffff) - (tpos[i+1] >> 31))
+  const float4* cell_tris;
+  const uint32_t* cell_tpos;
   const float4* gprims;     // (experiment DRT_GRID_INDEXED) each record once, Morton cell order, q2.w = index
   const uint32_t* cell_pos; // (experiment DRT_GRID_INDEXED) per reference: its record in gprims
   int gmacro_shift, gmacro_dim[3], gmacro_words;
@@ -155,6 +160,11 @@ struct FrameArgs {
   // MODE_REPLAY of an AA frame (pass 2 after MODE_CHAIN): no keyed-stream positions (skel_rk null);
   // reflections use MODE_AA's direction (the draws after the prologue never reach the frame, Q16)
   int aa_chain;
+  // Two-pass Whitted frames (round 5): the grid_res light samples of a pixel share its pixel-centre
+  // primary ray and every mirror bounce (main.cpp:683-696), so MODE_CHAIN traces one chain per pixel
+  // and MODE_REPLAY's sample slot i reads record i / chain_div (chain_div = grid_res; 1 for AA
+  // frames).  MODE_CHAIN counts chain_div samples per item.
+  int chain_div;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

@@ -212,9 +212,12 @@ typedef struct {
   int32_t tiles_in_shard;
   int32_t passes;      /* 2: a frame of a scene without refraction as a pass over the closest-hit
                           chains (in-order frames: a pixel's samples in order; AA frames of BVH / Grid
-                          scenes of >= 1024 objects, while the context's newest completed frame took
-                          >= 6 ms or none has completed) and a pass over every sample with its closest
-                          hits read back; 1 otherwise.  Both plans render the same frame. */
+                          scenes of >= 1024 objects whose whole frame has >= 2^23 samples or whose
+                          scene has >= 2^19 objects) and a pass over every sample with its closest
+                          hits read back; 1 otherwise.  The plan depends on the params and the
+                          uploaded scene only, and drt_render follows it.  Both plans render the
+                          same frame; the stats differ only in where shadow work is counted
+                          (shadow_* on the reference tree, wide_* on the shadow tree). */
   int32_t reserved[4];
 } drt_frame_plan;
 int drt_plan_frame(const drt_ctx* ctx, const drt_frame_params* params, drt_frame_plan* out);
@@ -269,6 +272,13 @@ int drt_frame_times(drt_ctx* ctx, int max_frames, double* path_ms, double* total
  * oldest frame returned: path-kernel start / end and frame end.  Frames on different streams
  * overlap; the union of their path-kernel spans is the device time the path kernel held. */
 int drt_frame_spans(drt_ctx* ctx, int max_frames, double* path_start, double* path_end, double* frame_end);
+/* The same frames' passes: a two-pass frame (drt_frame_plan.passes == 2) is the closest-chain pass
+ * then the replay pass, timed from the path-kernel start to the end of the first launch and from
+ * there to the path-kernel end (HIP events on the frame's stream; pass1 + pass2 = path_ms of
+ * drt_frame_times).  A one-pass frame reports its path kernel as pass 1 and 0 for pass 2.  For a
+ * frame rendered alone these are the launches' device times; with frames in flight a pass's span
+ * also holds its waits for CU room.  Waits for those frames.  Returns the count written (>= 0). */
+int drt_frame_pass_times(drt_ctx* ctx, int max_frames, double* pass1_ms, double* pass2_ms);
 
 /* ---- several GPUs behind one handle (main.cpp:603 is the loop being split) ----
  * One drt_ctx per device, one HIP stream per device and an RCCL clique over them

@@ -14,10 +14,10 @@ ROOT = Path(__file__).resolve().parents[1]
 if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
 
-# Two-pass AA frames (drt_capi.hip plan) are planned only while the context's last completed frame
-# took >= 6 ms; the parity tests render short frames and should cover the two-pass path, so they
-# lower the threshold to 0 (test_aa_two_pass_frame_time_rule checks the default rule itself).
-os.environ.setdefault("DRT_AA_TWO_PASS_MIN_MS", "0")
+# Two-pass AA frames (drt_capi.hip plan) are planned for frames of >= 2^23 samples or scenes of
+# >= 2^19 objects; the parity tests render small frames and should cover the two-pass path, so they
+# force it at every size (DRT_AA_TWO_PASS=2; test_aa_two_pass_size_rule checks the default rule).
+os.environ.setdefault("DRT_AA_TWO_PASS", "2")
 
 REFERENCE = Path("/root/reference/DistributionRayTracer")
 SCENES = REFERENCE / "P3D_Scenes"

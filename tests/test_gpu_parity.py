@@ -804,24 +804,32 @@ def test_aa_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, accel, kw
 
 
 @pytest.mark.parametrize("accel", ["bvh", "grid"])
-def test_aa_two_pass_frame_time_rule(drt, monkeypatch, accel):
-    """Short AA frames keep one pass (the second pass's tail costs ~0.5 ms per frame rendered alone):
-    a context plans two passes while none of its frames has completed or its newest completed frame
-    took >= DRT_AA_TWO_PASS_MIN_MS (default 6 ms).  Both plans render the same frame."""
+def test_aa_two_pass_size_rule(drt, monkeypatch, accel):
+    """Small AA frames keep one pass (the second pass's tail costs ~0.5 ms per frame rendered alone):
+    by default (DRT_AA_TWO_PASS=1) a frame is planned in two passes when the whole frame has >= 2^23
+    samples or the scene >= 2^19 objects.  The plan depends on the params and the scene only — the
+    same params plan the same way before and after frames complete — and both plans render the same
+    frame."""
     import bench
 
     s = drt.Scene()
     bench.populate(s, bench.synthetic_triangles(20_000), 64, 16, accel=accel)
     s.build()
-    monkeypatch.delenv("DRT_AA_TWO_PASS_MIN_MS")
+    monkeypatch.setenv("DRT_AA_TWO_PASS", "1")
     r = drt.Renderer(0)
     try:
         r.upload(s)
-        assert r.plan(r.frame_params(seed=3))["passes"] == 2  # no completed frame yet
-        two = r.render(seed=3)  # a 64 x 64 x 16 frame takes well under 6 ms
-        assert r.plan(r.frame_params(seed=3))["passes"] == 1
+        assert r.plan(r.frame_params(seed=3))["passes"] == 1  # 64 x 64 x 16 samples, 20 002 objects
         one = r.render(seed=3)
-        monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_MS", "0")
+        assert r.plan(r.frame_params(seed=3))["passes"] == 1  # no timing history
+        monkeypatch.setenv("DRT_AA_TWO_PASS_MIN_SAMPLES", str(64 * 64 * 16))
+        assert r.plan(r.frame_params(seed=3))["passes"] == 2
+        monkeypatch.delenv("DRT_AA_TWO_PASS_MIN_SAMPLES")
+        monkeypatch.setenv("DRT_AA_TWO_PASS_BIG_SCENE", "20002")
+        assert r.plan(r.frame_params(seed=3))["passes"] == 2
+        two = r.render(seed=3)
+        monkeypatch.delenv("DRT_AA_TWO_PASS_BIG_SCENE")
+        monkeypatch.setenv("DRT_AA_TWO_PASS", "2")
         assert r.plan(r.frame_params(seed=3))["passes"] == 2
         np.testing.assert_array_equal(bits(one), bits(two))
     finally:
@@ -869,3 +877,60 @@ def test_two_pass_in_order_frame_equals_one_pass(drt, renderer, tmp_path, monkey
     glass = sg.mixed_scene_text(res=(24, 16), spp=4, accel="bvh", n_tris=40, aperture=8.0, focal=1.5)
     renderer.upload(drt.Scene.load_p3f(sg.write(tmp_path, "glass.p3f", glass)))
     assert renderer.plan(renderer.frame_params(seed=5, roughness=0.1))["passes"] == 1
+
+
+@pytest.mark.parametrize("accel,first", [("bvh", "quad"), ("grid", "quad"), ("bvh", "point"), ("grid", "point")])
+def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, accel, first):
+    """Whitted frames (spp 0, main.cpp:674-703) of refraction-free scenes run in two passes (round 5):
+    the closest-chain pass traces ONE chain per pixel, because the grid_res light samples of a pixel
+    share its pixel-centre primary ray and every mirror bounce (main.cpp:683-696), and the replay pass
+    runs every (pixel, light sample) with that pixel's hits read back.  The frame equals the one-pass
+    frame (DRT_WHITTED_TWO_PASS=0) and the reference-order frame bit for bit, with the same samples
+    and shadow rays; a quad-light frame traverses grid_res times fewer closest-hit queries."""
+    import bench
+
+    s = drt.Scene()
+    c = bench.CAMERA
+    s.set_camera(c["eye"], c["at"], c["up"], c["fovy"], c["hither"], 48, 48, 0.0, 1.0)
+    s.set_background((0.078, 0.361, 0.753))
+    s.set_accel(accel)
+    s.set_spp(0)
+    quad = ((4, 3, 2), (1, 1, 1), (4, 2, 2), (3, 3, 2), 16)
+    if first == "quad":
+        s.add_light_quad(*quad)
+        s.add_light_point((-3, 1, 5), (1, 1, 1))
+    else:
+        s.add_light_point((-3, 1, 5), (1, 1, 1))
+        s.add_light_quad(*quad)
+    s.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), 0.5, 30.0827, 0, 1)
+    s.add_triangles(bench.synthetic_triangles(20_000))
+    s.build()
+    renderer.upload(s)
+    kw = {"max_depth": 6}
+    assert renderer.plan(renderer.frame_params(seed=4, **kw))["passes"] == 2
+    img = renderer.render(seed=4, stats=True, **kw)
+    st = renderer.stats()
+    monkeypatch.setenv("DRT_WHITTED_TWO_PASS", "0")
+    assert renderer.plan(renderer.frame_params(seed=4, **kw))["passes"] == 1
+    one = renderer.render(seed=4, stats=True, **kw)
+    st1 = renderer.stats()
+    ref = renderer.render(seed=4, stats=True, reference_order=True, **kw)
+    rst = renderer.stats()
+    np.testing.assert_array_equal(bits(img), bits(one))
+    np.testing.assert_array_equal(bits(img), bits(ref))
+    div = 16 if first == "quad" else 1
+    assert st["samples"] == st1["samples"] == rst["samples"] == 48 * 48 * div
+    assert st["shadow_rays"] == st1["shadow_rays"] == rst["shadow_rays"]
+    for k in ("closest_rays", "closest_inner", "closest_leaf", "closest_prims"):
+        assert st1[k] == rst[k], k
+        assert st[k] * div == st1[k], k
+    if accel == "grid":
+        for k in ("shadow_inner", "shadow_leaf", "shadow_prims"):
+            assert st[k] == st1[k] == rst[k], k
+    else:
+        assert st["wide_shadow_rays"] > 0.99 * st["shadow_rays"]
+    # the default rule: a quad-light Whitted frame takes two passes at any size, a point-light one by
+    # the AA frames' size rule (this 48 x 48 frame of 20 002 objects keeps one pass)
+    monkeypatch.delenv("DRT_WHITTED_TWO_PASS")
+    monkeypatch.setenv("DRT_AA_TWO_PASS", "1")
+    assert renderer.plan(renderer.frame_params(seed=4, **kw))["passes"] == (2 if first == "quad" else 1)

@@ -75,6 +75,9 @@ def main():
                 diff = float(np.mean(np.any(np.abs(gi - bi) > 1e-4, axis=2)))
                 print(json.dumps({"scene": name, "mode": mode, "res": list(s for s in gi.shape[1::-1]),
                                   "grid": g, "bvh": b, "grid_over_bvh": round(g["mrays_s"] / b["mrays_s"], 3),
+                                  # frame-time ratio (rays differ between one- and two-pass Whitted frames,
+                                  # whose light samples share one closest-hit chain per pixel)
+                                  "grid_speed_over_bvh": round(b["kernel_ms"] / g["kernel_ms"], 3),
                                   "grid_over_bvh_record_rate": round(g["record_GB_s"] / b["record_GB_s"], 3),
                                   "pixels_differing_frac": round(diff, 5)}), flush=True)
     r.close()

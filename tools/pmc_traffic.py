@@ -108,6 +108,8 @@ def main():
     out = Path(sys.argv[3]) if len(sys.argv) > 3 else ROOT / "profiles" / "pmc_traffic.json"
     sub = sys.argv[4] if len(sys.argv) > 4 else None
     vals, kernel = {}, None
+    pass_vals = [{}, {}]  # a two-pass frame's launches: the closest-chain pass, the replay pass
+    pass_kernels = [None, None]
     for p in sorted(x for x in root.iterdir() if x.is_dir()):
         c = dispatch_counters(p)
         k = timed_path_dispatch(c, sub)
@@ -121,6 +123,9 @@ def main():
             if prev:
                 p5 = max(prev)  # the frame's first pass
                 kernel = p5[1] + " + " + k[1]
+                pass_vals[0].update(c[p5])
+                pass_vals[1].update(c[k])
+                pass_kernels = [p5[1], k[1]]
                 for n, v in c[p5].items():
                     cur[n] = cur.get(n, 0.0) + v
         vals.update(cur)
@@ -128,6 +133,9 @@ def main():
     if "hbm_bytes_per_launch" not in rec:
         sys.exit(f"no read-byte counters under {root}: {sorted(vals)}")
     rec = {"kernel": kernel, **rec, "raw": vals}
+    if pass_kernels[0]:
+        # per pass (bench.py roofline.passes): the same derived figures for each launch on its own
+        rec["passes"] = [{"kernel": kn, **derive(pv), "raw": pv} for kn, pv in zip(pass_kernels, pass_vals)]
     db = {"workloads": {}}
     if out.exists():
         old = json.loads(out.read_text())
