@@ -107,6 +107,7 @@ struct drt_ctx {
   DevBuf d_cont_s[DRT_FRAME_SLOTS];
   // two-pass in-order frames: per sample slot its stream position, per slot and bounce its closest hit
   DevBuf d_skel_rk_s[DRT_FRAME_SLOTS], d_skel_hits_s[DRT_FRAME_SLOTS];
+  DevBuf d_heads_s[DRT_FRAME_SLOTS];  // replay passes: frame heads, max_depth + 1 per resident lane
   int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
@@ -721,7 +722,12 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   // 132 instead of 158 MB at 1M triangles.  A cell's list starts on a pair boundary: cell_tpos[i] is
   // its first record (even), bit 31 set when cell i - 1's list ended on a padding slot, so a cell's
   // range is [tpos[i], tpos[i + 1] - pad) from one 8-B load.
-  if (c->tri_only) {
+#ifdef DRT_GRID_RECS48
+  const bool packed = false;  // (A/B) the 48-B records for every scene
+#else
+  const bool packed = c->tri_only;
+#endif
+  if (packed) {
     std::vector<uint32_t> tpos(ncell + 1);
     uint64_t pos = 0;
     uint32_t pad = 0;
@@ -756,7 +762,7 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   }
   // other scenes' persistent Grid stepper reads the referenced records inline, in cell order (48 B
   // per reference; q2.w = the scene-order primitive index), so a cell's objects are one hop away
-  if (!c->tri_only) {
+  if (!packed) {
     std::vector<PrimRecord> recs((size_t)std::max<int64_t>(1, n_refs));
     for (int64_t i = 0; i < n_refs; i++) {
       recs[i] = c->prims_scene[o32[i]];
@@ -1083,12 +1089,18 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // Two-pass in-order frame: its closest-hit record is allocated first; a frame whose record does not
   // fit in device memory runs as the one-pass MODE_SEQ frame, which renders the same pixels.
   if (P.F.n_items && P.two_pass) {
+    // the replay pass's frame heads: max_depth + 1 per lane of every block the device can hold
+    // (<= 2048 threads per CU), indexed by the global thread id of the persistent grid
+    if (!c->cus) DRT_HIP(c, hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    const uint64_t head_bytes = sizeof(float4) * (uint64_t)std::max(1, c->cus) * 2048u * (uint64_t)(P.F.max_depth + 1);
     if ((!P.aa_chain && c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess) ||
         c->d_skel_hits_s[slot].ensure(sizeof(uint2) * (P.n_slots / P.chain_div) * (uint64_t)(P.F.max_depth + 1)) !=
-            hipSuccess) {
+            hipSuccess ||
+        c->d_heads_s[slot].ensure(head_bytes) != hipSuccess) {
       (void)hipGetLastError();
       c->d_skel_rk_s[slot].release();
       c->d_skel_hits_s[slot].release();
+      c->d_heads_s[slot].release();
       P.two_pass = P.aa_chain = false;
     }
   }
@@ -1216,7 +1228,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DRT_HIP(c, hipGetLastError());
     DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
-    F2.mode = MODE_REPLAY;
+    F2.mode = P.aa_chain ? MODE_AREPLAY : MODE_REPLAY;
+    F2.heads = c->d_heads_s[slot].as<float4>();
     F2.nsub = P.F.nsub;
     F2.waves = env_int("DRT_REPLAY_WAVES", P.F.waves);
     F2.process_min = env_int("DRT_REPLAY_PROCESS_MIN", P.F.process_min);  // 12 / 40: 1 861 / 1 764 vs 1 897

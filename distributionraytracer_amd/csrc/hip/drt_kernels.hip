@@ -819,10 +819,10 @@ __device__ __forceinline__ bool ray_finite(const RayP& r) {
   return inv_finite(r) && fabsf(r.o.x) < __builtin_inff() && fabsf(r.o.y) < __builtin_inff() &&
          fabsf(r.o.z) < __builtin_inff();
 }
-// Shadow-tree lanes (the one-fma child test's range, node_step): |inv| <= 2^40 (no direction
-// component below ~1e-12 of the ray's length) and |o| <= 2^60.  Other rays walk the binary tree.
+// Shadow-tree lanes: finite rays; with the one-fma child test (DRT_WIDE_FMA1, node_step) also |inv| <=
+// 2^40 (no direction component below ~1e-12 of the ray's length) and |o| <= 2^60.
 __device__ __forceinline__ bool wide_ray_ok(const RayP& r) {
-#ifdef DRT_WIDE_EXACT
+#ifndef DRT_WIDE_FMA1
   return ray_finite(r);
 #else
   const float mi = fmaxf(fmaxf(fabsf(r.ix), fabsf(r.iy)), fabsf(r.iz));
@@ -928,6 +928,15 @@ __device__ __forceinline__ DdaState dda_step(DdaState d, const DdaAxes& a, bool 
 // in two VGPRs, so that the walk also steps through the empty cells of non-empty macro-cells
 // (36-48 % of their cells) without loading their ranges: bit-identical, but VGPR spills 102 ->
 // 115 and 1 047 against 1 300 Mrays/s; 3-11 % slower on the shipped Grid scenes too.)
+// triangle scenes read the 40-B pair layout (drt_upload_grid); -DDRT_GRID_RECS48 keeps the 48-B
+// records for every scene (A/B)
+template <bool TRI_ONLY>
+constexpr bool kGridPacked =
+#ifdef DRT_GRID_RECS48
+    false;
+#else
+    TRI_ONLY;
+#endif
 template <bool TRI_ONLY, bool STATS>
 __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters& C, const LdsU32* macro, int walk,
                                           int pairs) {
@@ -941,8 +950,8 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
   uint32_t b = 0, e = 0;  // LF_EMPTY: the cell lies in an empty macro-cell (the last call's walk)
   if (!(fl & LF_EMPTY)) {  // the cell's range [start, next start) in one 8-B load (4-B aligned)
     uint2 r;
-    __builtin_memcpy(&r, (TRI_ONLY ? S.cell_tpos : S.cell_start) + cidx, sizeof(r));
-    if (TRI_ONLY) {  // pair-aligned starts; bit 31 of the next start: this list ends on a padding slot
+    __builtin_memcpy(&r, (kGridPacked<TRI_ONLY> ? S.cell_tpos : S.cell_start) + cidx, sizeof(r));
+    if (kGridPacked<TRI_ONLY>) {  // pair-aligned starts; bit 31 of the next start: this list ends on a padding slot
       r.x &= 0x7fffffffu;
       r.y = (r.y & 0x7fffffffu) - (r.y >> 31);
     }
@@ -1001,7 +1010,7 @@ __device__ __forceinline__ void grid_step(const SceneArgs& S, Lane& L, Counters&
     }
 #else
     float4 a0, a1, a2, c0, c1, c2;
-    if (TRI_ONLY) {  // a pair of 40-B triangle records (q is even): five 16-B loads, three for one
+    if (kGridPacked<TRI_ONLY>) {  // a pair of 40-B triangle records (q is even): five 16-B loads, three for one
       const float4* r = S.cell_tris + 5 * (size_t)(q >> 1);
       const float4 x0 = r[0], x1 = r[1], x2 = r[2];
       float4 x3, x4;
@@ -1234,8 +1243,8 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
         tn[2 * h + j] = t0;
       }
     }
-#elif !defined(DRT_WIDE_EXACT)
-    // Round 5: each plane as ONE fma, t = q * S + B with B = (p - o) * inv and S = 2^E * inv per axis
+#elif defined(DRT_WIDE_FMA1)
+    // (A/B, round 5; kept out) each plane as ONE fma, t = q * S + B with B = (p - o) * inv and S = 2^E * inv per axis
     // and node, instead of (fma(q, 2^E, p) - o) * inv (two more VALU per plane, 48 per node).  The
     // value is not the reference arithmetic's on the decoded plane, so the test is widened by a
     // bound on the difference: with M = max over axes of |B| + 255 |S| >= every |t| of
@@ -1265,7 +1274,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       hk[k] = fmaxf(t0, 0.0f) < t1 + D2;
       tn[k] = t0;
     }
-#else  // DRT_WIDE_EXACT (A/B): the reference arithmetic on the decoded planes
+#else  // the reference arithmetic on the decoded planes
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int sh = 8 * k;
@@ -1459,12 +1468,18 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
 }
 
 // Path-kernel modes whose shadow queries walk the 4-ary shadow tree (see the node loop).
+// MODE_REPLAY: an in-order frame's replay (keyed-stream draws from recorded positions); MODE_AREPLAY:
+// an AA / Whitted frame's replay (no draw after the prologue reaches the frame, so no RNG, DoF or
+// stream positions in its code: L.rk holds the sample's closest-chain record instead)
+template <int MODE>
+constexpr bool kReplay = MODE == MODE_REPLAY || MODE == MODE_AREPLAY;
+
 template <int MODE>
 constexpr bool kPathWide =
 #ifdef DRT_PATH_WIDE
     MODE != MODE_SKEL;
 #else
-    MODE == MODE_REPLAY;
+    kReplay<MODE>;
 #endif
 
 template <bool STATS, int ACC, int MODE>
@@ -1492,7 +1507,6 @@ template <int MODE>
 __device__ __forceinline__ V3 reflect_dir(const FrameArgs& F, Lane& L, V3 N, V3 V) {
   V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
   if (MODE == MODE_SEQ || MODE == MODE_PROG || MODE == MODE_SKEL || MODE == MODE_REPLAY) {
-    if (MODE == MODE_REPLAY && F.aa_chain) return normalize(R);  // an AA frame's replay: MODE_AA's reflection
     KRng rng{F.seed, L.pmix, L.rk};
     R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
     L.rk = rng.k;
@@ -1509,9 +1523,10 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
 template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void closest_query(const SceneArgs& S, const FrameArgs& F, Lane& L, const RayP& q,
                                               Counters& C) {
-  if (MODE == MODE_REPLAY) {
-    // a Whitted frame's light samples share their pixel's record (FrameArgs::chain_div)
-    const uint32_t rec = F.chain_div > 1 ? L.item / (uint32_t)F.chain_div : L.item;
+  if (kReplay<MODE>) {
+    // an AA / Whitted frame's replay keeps its record index in L.rk (lane_init; a Whitted frame's
+    // light samples share their pixel's record, FrameArgs::chain_div), an in-order frame's is the item
+    const uint32_t rec = MODE == MODE_AREPLAY ? L.rk : L.item;
     const uint2 h = F.skel_hits[(size_t)rec * (uint32_t)(F.max_depth + 1) + (uint32_t)(L.depth - 1)];
     L.q = q;
     L.best_t = __uint_as_float(h.x);
@@ -1542,6 +1557,23 @@ struct FrameStack {
   FrameHead h[kMaxFrames];
   FrameTail t[kMaxFrames];
 };
+
+// Round 5: a replay pass (no refraction: every parent is a mirror parent) keeps its frame heads in
+// global memory, each lane's run of max_depth + 1 heads contiguous (FrameArgs::heads), one 16-B record
+// per frame: (acc, material | flags << 24).  The private FrameStack is lane-interleaved scratch: a
+// 24-B head store by a lane of a partly active shading wave wrote six partly filled sectors
+// (C4: 76 GB of the replay pass's writes per frame).  -DDRT_HEADS_SCRATCH keeps the FrameStack (A/B).
+template <int MODE, int ACC>
+constexpr bool kReplayHeads =
+#ifdef DRT_HEADS_SCRATCH
+    false;
+#else
+    kReplay<MODE> && ACC == ACC_BVH;  // (the Grid replay measured 7 % slower with them: 28 -> 50 spills)
+#endif
+__device__ __forceinline__ float4* replay_head(const FrameArgs& F, uint32_t fsp) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  return F.heads + (size_t)lane * (uint32_t)(F.max_depth + 1) + fsp;
+}
 
 // MODE_SEQ tail: hand the rest of the lane's pixel (next sample L.smp, keyed-stream position
 // L.rk) to another wave through a continuation slot.  One 64-bit word per slot, written and read
@@ -1643,7 +1675,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       const float sin_t = eta * sin_i;
       // MODE_REPLAY frames have no refracting material (the two-pass plan's condition): no refraction
       // child, Fresnel or Beer code and no frame tails in that instantiation
-      const bool has_refr = MODE != MODE_REPLAY && (m.trans == 1.0f && sin_t < 1.0f);
+      const bool has_refr = !kReplay<MODE> && (m.trans == 1.0f && sin_t < 1.0f);
       const bool has_refl = m.ks > 0.0f;
       V3 beer = mk(1.f, 1.f, 1.f);
       RayP child = L.q;
@@ -1666,7 +1698,19 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       } else if (m.trans > 0.0f && sin_t >= 1.0f) {
         kr = 1.0f;
       }
-      if (has_refr || has_refl) {
+      if (kReplayHeads<MODE, ACC> && has_refl) {
+        // a replay's frame head: one 16-B store to the lane's own run (replay_head), kr rebuilt from
+        // the material and bit 4 at the unwind
+        const V3 R = reflect_dir<MODE>(F, L, L.N, L.V);
+        const uint32_t flags = 1u | (outside ? 2u : 0u) | 4u | (dot(R, L.N) > 0.0f ? 8u : 0u) | (kr == 1.0f && m.refl != 1.0f ? 16u : 0u);
+        *replay_head(F, L.fsp) = make_float4(L.acc.x, L.acc.y, L.acc.z, __uint_as_float(L.mat | (flags << 24)));
+        L.fsp++;
+        L.ls = L.lightPos;
+        L.depth++;
+        closest_query<STATS, MODE, ACC>(S, F, L, make_ray(add(L.hitP, mul(L.N, offset)), R), C);
+        return;
+      }
+      if (!kReplayHeads<MODE, ACC> && (has_refr || has_refl)) {
         FrameHead& f = fs.h[L.fsp];
         f.acc = L.acc; f.kr = kr; f.mat = L.mat;
         uint32_t flags = (has_refr ? 0u : 1u) | (outside ? 2u : 0u) | (has_refl ? 4u : 0u);
@@ -1686,7 +1730,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
         L.depth++;
         closest_query<STATS, MODE, ACC>(S, F, L, child, C);
 #ifdef DRT_REPLAY_CHAIN
-        if (MODE == MODE_REPLAY) goto again;
+        if (kReplay<MODE>) goto again;
 #endif
         return;
       }
@@ -1698,10 +1742,23 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
   // continues with its reflection child.  The Grid stepper keeps the store-through form (each
   // frame updated in place): with the register-only form its allocation changed, 605 -> 510
   // Mrays/s, while the BVH kernel gained 1.5 %.
-  if (ACC == ACC_GRID) {
+  if (kReplayHeads<MODE, ACC>) {  // a replay's frames: mirror parents only (main.cpp:513-518)
+    while (L.fsp > 0) {
+      const float4 h = *replay_head(F, L.fsp - 1);
+      const uint32_t w = __float_as_uint(h.w), flags = w >> 24, mat = w & 0xffffffu;
+      V3 acc = mk(h.x, h.y, h.z);
+      if (flags & 8u) {
+        const float kr = (flags & 16u) ? 1.0f : S.mats[mat].refl;
+        acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(S.mats[mat].spec)));
+      }
+      c = cclamp(acc);
+      L.fsp--;
+    }
+  }
+  if (!kReplayHeads<MODE, ACC> && ACC == ACC_GRID) {
     while (L.fsp > 0) {
       FrameHead& f = fs.h[L.fsp - 1];
-      if (MODE != MODE_REPLAY && (f.flags & 1u) == 0u) {
+      if (!kReplay<MODE> && (f.flags & 1u) == 0u) {
         const FrameTail& ft = fs.t[L.fsp - 1];
         V3 rc = cclamp(c);
         if ((f.flags & 2u) == 0u) rc = cmulc(rc, ft.beer);
@@ -1727,12 +1784,12 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       }
     }
   }
-  while (ACC != ACC_GRID && L.fsp > 0) {
+  while (!kReplayHeads<MODE, ACC> && ACC != ACC_GRID && L.fsp > 0) {
     FrameHead& f = fs.h[L.fsp - 1];
     const uint32_t flags = f.flags;
     V3 acc = f.acc;
     const float kr = f.kr;
-    if (MODE != MODE_REPLAY && (flags & 1u) == 0u) {  // refraction child returned (main.cpp:489-496)
+    if (!kReplay<MODE> && (flags & 1u) == 0u) {  // refraction child returned (main.cpp:489-496)
       const FrameTail& ft = fs.t[L.fsp - 1];
       V3 rc = cclamp(c);
       if ((flags & 2u) == 0u) rc = cmulc(rc, ft.beer);
@@ -1817,13 +1874,13 @@ __device__ void chain_process(const SceneArgs& S, const FrameArgs& F, Lane& L, C
 template <bool STATS, int MODE, int ACC>
 __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
   // MODE_REPLAY lanes hold a sample slot (pixel * nsub + sample), the others a pixel
-  const uint32_t pixel = MODE == MODE_REPLAY ? L.item / (uint32_t)F.nsub : L.item;
+  const uint32_t pixel = kReplay<MODE> ? L.item / (uint32_t)F.nsub : L.item;
   const Item it = decode_item(F, S.res_x, S.res_y, pixel, 1);
   L.depth = 1;
   L.fsp = 0;
   L.ior1 = 1.0f;
   L.fl = 0u;
-  if (STATS && MODE != MODE_REPLAY) C.v[ST_SAMPLES]++;  // pass 1 counts the two-pass frame's samples
+  if (STATS && !kReplay<MODE>) C.v[ST_SAMPLES]++;  // pass 1 counts the two-pass frame's samples
   if (MODE == MODE_SKEL) F.skel_rk[(size_t)L.item * F.nsub + L.smp] = L.rk;
   RayP r;
   if (F.spp > 0) {
@@ -1831,7 +1888,7 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
     const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + L.smp] : shuffle_source(F, L.pmix, (int)L.smp);
     sample_prologue_at(F, L.pmix, (int)L.smp, pos, rx, ry, sx, sy);
     const float px = (float)it.x + rx, py = (float)it.y + ry;
-    if (F.dof) {
+    if (MODE != MODE_AREPLAY && F.dof) {  // (an AA frame's replay has no DoF: those frames are in-order)
       KRng rng{F.seed, L.pmix, L.rk};
       r = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
       L.rk = rng.k;
@@ -1880,7 +1937,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     seq_begin<STATS, MODE, ACC>(S, F, L, item, 0u, seq_first_rk(F), C);
     return;
   }
-  if (MODE == MODE_REPLAY) {  // work item = sample slot: the sample from its recorded stream position
+  if (kReplay<MODE>) {  // work item = sample slot: the sample from its recorded stream position
     const Item it = decode_item(F, S.res_x, S.res_y, item, F.nsub);
     if (!it.valid) {  // padding of a partial tile
       F.samples[item] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1889,7 +1946,10 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     }
     L.pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     L.smp = (uint32_t)it.sub;
-    L.rk = F.skel_rk ? F.skel_rk[item] : 0u;  // an AA frame's replay has no stream positions
+    // an AA / Whitted frame's replay has no stream positions (no draw after the prologue reaches the
+    // frame, Q16): its rk holds the sample's closest-chain record instead (closest_query)
+    L.rk = MODE == MODE_REPLAY ? F.skel_rk[item]
+                               : (F.chain_div > 1 ? ((uint32_t)item - (uint32_t)it.sub) / (uint32_t)F.chain_div : item);
     seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
     return;
   }
@@ -2108,7 +2168,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
 #else
         constexpr int kLeaf1 =
-            !TRI_ONLY || MODE == MODE_REPLAY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
+            !TRI_ONLY || kReplay<MODE> || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
 #endif
         // The shadow tree stays out of the path kernel (measured, round 4, headline 512^2 x 64 spp): its
         // lanes walked 26 % fewer node records per ray (75.8 -> 56.2 visits), but a wave whose lanes
@@ -2452,7 +2512,7 @@ static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStrea
   // (MODE_SKEL, the closest-chain pass, carries little state: 4 spills at 6 waves.  Measured at 4, 5,
   // 7 and 8 waves/SIMD on C4: 305, 280, 554 and 760 ms against 278 ms at 6.)
 #ifdef DRT_REPLAY_LOW_WAVES
-  if constexpr (M == MODE_REPLAY) {
+  if constexpr (kReplay<M>) {
     if (F.waves == 5) return launch_persistent_w<T, ST, M, 5, A>(S, F, st);
     if (F.waves == 4) return launch_persistent_w<T, ST, M, 4, A>(S, F, st);
   }
@@ -2468,6 +2528,7 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
     case MODE_SEQ: launch_persistent_m<T, ST, MODE_SEQ, A>(S, F, st); break;
     case MODE_SKEL: launch_persistent_m<T, ST, MODE_SKEL, A>(S, F, st); break;
     case MODE_REPLAY: launch_persistent_m<T, ST, MODE_REPLAY, A>(S, F, st); break;
+    case MODE_AREPLAY: launch_persistent_m<T, ST, MODE_AREPLAY, A>(S, F, st); break;
     case MODE_CHAIN: launch_persistent_m<T, ST, MODE_CHAIN, A>(S, F, st); break;
     case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG, A>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT, A>(S, F, st); break;

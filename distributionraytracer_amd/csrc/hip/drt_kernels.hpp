@@ -24,9 +24,12 @@ enum FrameMode : int {
                     // rays traced
   // An AA frame (MODE_AA) of a refraction-free BVH scene in two passes (round 4), so that the
   // shadow queries run in waves of shadow queries only, on the 4-ary shadow tree:
-  MODE_CHAIN = 7    // pass 1, one lane per (pixel, sample): the sample's closest-hit chain only,
+  MODE_CHAIN = 7,   // pass 1, one lane per (pixel, sample): the sample's closest-hit chain only,
                     // each bounce's hit recorded; pass 2 is MODE_REPLAY.  A Whitted frame (spp 0,
                     // round 5) in two passes: one lane per pixel, the chain its light samples share
+  MODE_AREPLAY = 8  // pass 2 of an AA / Whitted frame (round 5: its own instantiation; MODE_REPLAY
+                    // stays the in-order frames'): no keyed-stream draw after the prologue reaches
+                    // the frame, so no RNG, DoF or stream positions in its code
 };
 
 enum StatSlot : int {
@@ -165,6 +168,9 @@ struct FrameArgs {
   // and MODE_REPLAY's sample slot i reads record i / chain_div (chain_div = grid_res; 1 for AA
   // frames).  MODE_CHAIN counts chain_div samples per item.
   int chain_div;
+  // replay passes: frame heads, max_depth + 1 float4 per resident lane (blockIdx * blockDim +
+  // threadIdx), each lane's run contiguous
+  float4* heads;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

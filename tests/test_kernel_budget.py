@@ -30,15 +30,19 @@ BUDGET = {
     # Whitted point-light frames on mixed primitives (the shipped Whitted scenes on a BVH)
     "drt::path_persistent<false, false, 3, 6, 2>": (80, 2336, 6, 65),
     # C4 as two passes (round 3): the closest-chain pass, and the per-sample replay without refraction
+    # (round 5: its frame heads in lane-contiguous global memory, not scratch: 2 224 -> 880 B)
     "drt::path_persistent<true, false, 5, 6, 2>": (80, 704, 6, 5),
-    "drt::path_persistent<true, false, 6, 6, 2>": (80, 2224, 6, 45),
-    # round 4: the headline's AA frame in two passes — its closest-chain pass (the replay above is
-    # the other, its shadow queries on the 4-ary shadow tree: 42 -> 45 spills with that step)
+    "drt::path_persistent<true, false, 6, 6, 2>": (80, 880, 6, 39),
+    # round 4: the headline's AA frame in two passes — its closest-chain pass, and (round 5: its own
+    # instantiation, MODE_AREPLAY, no RNG code; frame heads in global memory) its replay pass
     "drt::path_persistent<true, false, 7, 6, 2>": (80, 704, 6, 2),
+    "drt::path_persistent<true, false, 8, 6, 2>": (80, 800, 6, 36),
     # batched shadow queries (drt_trace_shadow) on the 4-ary shadow tree: 8 waves/SIMD, no spills
     "drt::trace_stream<true, 2, 6, false>": (64, 352, 8, 0),
-    # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs)
+    # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs), and the two passes of the Grid headline's frame
     "drt::path_persistent<true, false, 0, 5, 1>": (96, 1844, 5, 230),
+    "drt::path_persistent<true, false, 7, 5, 1>": (96, 8, 5, 1),
+    "drt::path_persistent<true, false, 8, 5, 1>": (96, 1524, 5, 28),
 }
 
 

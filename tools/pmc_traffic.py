@@ -118,7 +118,7 @@ def main():
         kernel = k[1]
         cur = dict(c[k])
         # a two-pass frame (FrameMode 5 or 7, then 6, drt_capi.hip): the frame is both launches
-        if _mode(k[1]) == 6:
+        if _mode(k[1]) in (6, 8):
             prev = [d for d in c if d[0] < k[0] and _mode(d[1]) in (5, 7) and not _stats(d[1])]
             if prev:
                 p5 = max(prev)  # the frame's first pass
