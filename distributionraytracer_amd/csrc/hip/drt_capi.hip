@@ -1089,14 +1089,15 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   // Two-pass in-order frame: its closest-hit record is allocated first; a frame whose record does not
   // fit in device memory runs as the one-pass MODE_SEQ frame, which renders the same pixels.
   if (P.F.n_items && P.two_pass) {
-    // the replay pass's frame heads: max_depth + 1 per lane of every block the device can hold
-    // (<= 2048 threads per CU), indexed by the global thread id of the persistent grid
+    // the in-order BVH replay pass's frame heads (kReplayHeads): max_depth + 1 per lane of every block
+    // the device can hold (<= 2048 threads per CU), indexed by the global thread id of the persistent grid
     if (!c->cus) DRT_HIP(c, hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    const bool heads = !P.aa_chain && c->accel == DRT_ACCEL_BVH;
     const uint64_t head_bytes = sizeof(float4) * (uint64_t)std::max(1, c->cus) * 2048u * (uint64_t)(P.F.max_depth + 1);
     if ((!P.aa_chain && c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess) ||
         c->d_skel_hits_s[slot].ensure(sizeof(uint2) * (P.n_slots / P.chain_div) * (uint64_t)(P.F.max_depth + 1)) !=
             hipSuccess ||
-        c->d_heads_s[slot].ensure(head_bytes) != hipSuccess) {
+        (heads && c->d_heads_s[slot].ensure(head_bytes) != hipSuccess)) {
       (void)hipGetLastError();
       c->d_skel_rk_s[slot].release();
       c->d_skel_hits_s[slot].release();
@@ -1229,7 +1230,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
     F2.mode = P.aa_chain ? MODE_AREPLAY : MODE_REPLAY;
-    F2.heads = c->d_heads_s[slot].as<float4>();
+    F2.heads = (!P.aa_chain && c->accel == DRT_ACCEL_BVH) ? c->d_heads_s[slot].as<float4>() : nullptr;
     F2.nsub = P.F.nsub;
     F2.waves = env_int("DRT_REPLAY_WAVES", P.F.waves);
     F2.process_min = env_int("DRT_REPLAY_PROCESS_MIN", P.F.process_min);  // 12 / 40: 1 861 / 1 764 vs 1 897

@@ -1558,17 +1558,21 @@ struct FrameStack {
   FrameTail t[kMaxFrames];
 };
 
-// Round 5: a replay pass (no refraction: every parent is a mirror parent) keeps its frame heads in
-// global memory, each lane's run of max_depth + 1 heads contiguous (FrameArgs::heads), one 16-B record
-// per frame: (acc, material | flags << 24).  The private FrameStack is lane-interleaved scratch: a
-// 24-B head store by a lane of a partly active shading wave wrote six partly filled sectors
+// Round 5: the in-order frames' replay pass (no refraction: every parent is a mirror parent) keeps its
+// frame heads in global memory, each lane's run of max_depth + 1 heads contiguous (FrameArgs::heads),
+// one 16-B record per frame: (acc, material | flags << 24).  The private FrameStack is lane-interleaved
+// scratch: a 24-B head store by a lane of a partly active shading wave wrote six partly filled sectors
 // (C4: 76 GB of the replay pass's writes per frame).  -DDRT_HEADS_SCRATCH keeps the FrameStack (A/B).
 template <int MODE, int ACC>
 constexpr bool kReplayHeads =
 #ifdef DRT_HEADS_SCRATCH
     false;
 #else
-    kReplay<MODE> && ACC == ACC_BVH;  // (the Grid replay measured 7 % slower with them: 28 -> 50 spills)
+    // the in-order frames' replay (C4: replay writes 70.0 -> 37.3 GB per frame, same speed); the AA /
+    // Whitted replay measured 0.6 % faster with the scratch FrameStack on the headline (1 969-1 977
+    // against 1 964-1 966 Mrays/s; its writes 10.7 against 5.5 GB), and the Grid's 7 % faster (28
+    // against 50 VGPR spills; profiles/r05_ab_*)
+    MODE == MODE_REPLAY && ACC == ACC_BVH;
 #endif
 __device__ __forceinline__ float4* replay_head(const FrameArgs& F, uint32_t fsp) {
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;

@@ -34,9 +34,9 @@ BUDGET = {
     "drt::path_persistent<true, false, 5, 6, 2>": (80, 704, 6, 5),
     "drt::path_persistent<true, false, 6, 6, 2>": (80, 880, 6, 39),
     # round 4: the headline's AA frame in two passes — its closest-chain pass, and (round 5: its own
-    # instantiation, MODE_AREPLAY, no RNG code; frame heads in global memory) its replay pass
+    # instantiation, MODE_AREPLAY, no RNG code: 45 -> 35 spills) its replay pass
     "drt::path_persistent<true, false, 7, 6, 2>": (80, 704, 6, 2),
-    "drt::path_persistent<true, false, 8, 6, 2>": (80, 800, 6, 36),
+    "drt::path_persistent<true, false, 8, 6, 2>": (80, 2224, 6, 35),
     # batched shadow queries (drt_trace_shadow) on the 4-ary shadow tree: 8 waves/SIMD, no spills
     "drt::trace_stream<true, 2, 6, false>": (64, 352, 8, 0),
     # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs), and the two passes of the Grid headline's frame
