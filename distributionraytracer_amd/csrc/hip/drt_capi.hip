@@ -908,6 +908,8 @@ struct Plan {
   bool two_pass;        // in-order frame as MODE_SKEL + MODE_REPLAY (no refraction in the scene)
   bool aa_chain;        // ... or an AA frame as MODE_CHAIN + MODE_REPLAY (BVH, shadow tree uploaded)
   uint32_t chain_div;   // two-pass Whitted frame: replay sample slots per closest-chain record (grid_res)
+  bool tree;            // ... of a scene with a refracting material: MODE_TCHAIN + MODE_TREPLAY
+  uint32_t recs;        // closest-hit records per (shared) sample: max_depth + 1, or 2^(max_depth+1) - 1
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -1023,9 +1025,7 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) &&
       !(p->flags & DRT_FRAME_REFERENCE_ORDER) && aa2 != 0 &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
-    bool refr = false;
-    for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
-    P.two_pass = P.aa_chain = !refr;
+    P.two_pass = P.aa_chain = true;
   }
   // Whitted frames in two passes too (round 5): the closest-chain pass traces ONE chain per pixel —
   // its grid_res light samples share the pixel-centre primary ray and every mirror bounce
@@ -1041,10 +1041,32 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
       (F.mode == MODE_WHITTED_QUAD ? F.grid_res >= 4 || aa2 >= 2 : big_frame) &&
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) && !(p->flags & DRT_FRAME_REFERENCE_ORDER) &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
+    P.two_pass = P.aa_chain = true;
+    P.chain_div = F.mode == MODE_WHITTED_QUAD ? (uint32_t)F.nsub : 1u;
+  }
+  // A scene with a refracting material (trans == 1, main.cpp:471) makes a sample's closest hits a
+  // binary tree (refraction child first, then reflection): its AA / Whitted frames take two passes as
+  // MODE_TCHAIN (every closest hit of the tree, recorded in rayTracing()'s query order, no shadow
+  // rays) + MODE_TREPLAY (the whole rayTracing() with the hits read back in that order), when the
+  // record — up to 2^(max_depth + 1) - 1 hits per sample — fits (round 5; DRT_TREE_TWO_PASS=0: one
+  // pass).  Otherwise one pass, as before.
+  P.tree = false;
+  P.recs = (uint32_t)md + 1u;
+  if (P.aa_chain) {
     bool refr = false;
     for (const drt_material& m : c->mats) refr = refr || m.trans == 1.0f;
-    P.two_pass = P.aa_chain = !refr;
-    P.chain_div = F.mode == MODE_WHITTED_QUAD ? (uint32_t)F.nsub : 1u;
+    if (refr) {
+      const uint64_t recs = (1ull << (md + 1)) - 1ull;
+      const uint64_t shared = P.n_slots / P.chain_div;
+      if (env_int("DRT_TREE_TWO_PASS", 1) != 0 && md <= 12 && shared * recs * 8u <= kTwoPassMaxBytes &&
+          shared * recs < 0xFFFFFFFFull) {
+        P.tree = true;
+        P.recs = (uint32_t)recs;
+      } else {
+        P.two_pass = P.aa_chain = false;
+        P.chain_div = 1;
+      }
+    }
   }
   ReduceArgs& R = P.R;
   R.nsub = slots;
@@ -1095,14 +1117,13 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     const bool heads = !P.aa_chain && c->accel == DRT_ACCEL_BVH;
     const uint64_t head_bytes = sizeof(float4) * (uint64_t)std::max(1, c->cus) * 2048u * (uint64_t)(P.F.max_depth + 1);
     if ((!P.aa_chain && c->d_skel_rk_s[slot].ensure(sizeof(uint32_t) * P.n_slots) != hipSuccess) ||
-        c->d_skel_hits_s[slot].ensure(sizeof(uint2) * (P.n_slots / P.chain_div) * (uint64_t)(P.F.max_depth + 1)) !=
-            hipSuccess ||
+        c->d_skel_hits_s[slot].ensure(sizeof(uint2) * (P.n_slots / P.chain_div) * (uint64_t)P.recs) != hipSuccess ||
         (heads && c->d_heads_s[slot].ensure(head_bytes) != hipSuccess)) {
       (void)hipGetLastError();
       c->d_skel_rk_s[slot].release();
       c->d_skel_hits_s[slot].release();
       c->d_heads_s[slot].release();
-      P.two_pass = P.aa_chain = false;
+      P.two_pass = P.aa_chain = P.tree = false;
     }
   }
   // MODE_SEQ tail hand-over (DRT_SEQ_DONATE: 0 off, 1 on, default auto).  It frees whole blocks
@@ -1199,7 +1220,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DevBuf& d_rk = c->d_skel_rk_s[slot];  // allocated above
     DevBuf& d_hits = c->d_skel_hits_s[slot];
     FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order (AA: any order)
-    F1.mode = P.aa_chain ? MODE_CHAIN : MODE_SKEL;
+    F1.mode = P.tree ? MODE_TCHAIN : (P.aa_chain ? MODE_CHAIN : MODE_SKEL);
+    F1.tree_recs = (int)P.recs;
     F1.skel_rk = P.aa_chain ? nullptr : d_rk.as<uint32_t>();
     F1.skel_hits = d_hits.as<uint2>();
     F1.aa_chain = P.aa_chain ? 1 : 0;
@@ -1229,7 +1251,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     DRT_HIP(c, hipGetLastError());
     DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
-    F2.mode = P.aa_chain ? MODE_AREPLAY : MODE_REPLAY;
+    F2.mode = P.tree ? MODE_TREPLAY : (P.aa_chain ? MODE_AREPLAY : MODE_REPLAY);
     F2.heads = (!P.aa_chain && c->accel == DRT_ACCEL_BVH) ? c->d_heads_s[slot].as<float4>() : nullptr;
     F2.nsub = P.F.nsub;
     F2.waves = env_int("DRT_REPLAY_WAVES", P.F.waves);

@@ -1473,13 +1473,16 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
 // stream positions in its code: L.rk holds the sample's closest-chain record instead)
 template <int MODE>
 constexpr bool kReplay = MODE == MODE_REPLAY || MODE == MODE_AREPLAY;
+// passes that read their closest hits back (kReplay: refraction-free frames; MODE_TREPLAY: a hit tree)
+template <int MODE>
+constexpr bool kReadBack = kReplay<MODE> || MODE == MODE_TREPLAY;
 
 template <int MODE>
 constexpr bool kPathWide =
 #ifdef DRT_PATH_WIDE
     MODE != MODE_SKEL;
 #else
-    kReplay<MODE>;
+    kReadBack<MODE>;
 #endif
 
 template <bool STATS, int ACC, int MODE>
@@ -1523,6 +1526,14 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
 template <bool STATS, int MODE, int ACC>
 __device__ __forceinline__ void closest_query(const SceneArgs& S, const FrameArgs& F, Lane& L, const RayP& q,
                                               Counters& C) {
+  if (MODE == MODE_TREPLAY) {  // the sample's next closest hit, in the order pass 1 recorded them
+    const uint2 h = F.skel_hits[L.rk++];
+    L.q = q;
+    L.best_t = __uint_as_float(h.x);
+    L.best_prim = h.y;
+    L.fl = (L.fl & LF_OUTSIDE) | (h.y != 0xFFFFFFFFu ? LF_HIT : 0u);
+    return;
+  }
   if (kReplay<MODE>) {
     // an AA / Whitted frame's replay keeps its record index in L.rk (lane_init; a Whitted frame's
     // light samples share their pixel's record, FrameArgs::chain_div), an in-order frame's is the item
@@ -1615,7 +1626,7 @@ __device__ __forceinline__ void finish_sample(const SceneArgs& S, const FrameArg
     L.item = kNoItem;
     return;
   }
-  F.samples[L.item] = make_float4(c.x, c.y, c.z, 0.0f);
+  if (MODE != MODE_TCHAIN) F.samples[L.item] = make_float4(c.x, c.y, c.z, 0.0f);  // (pass 2 writes it)
   L.item = kNoItem;
 }
 
@@ -1630,11 +1641,13 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
   V3 c = mk(0, 0, 0);
   bool after_lights = false;
   const bool hit = (L.fl & LF_HIT) != 0u;
+  if (MODE == MODE_TCHAIN && !(L.fl & LF_SHADOW))  // pass 1 of a refracting frame: record the hit
+    F.skel_hits[L.rk++] = make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
   if (MODE == MODE_SEQ && (L.fl & LF_RESUME)) {
     // a handed-over pixel: no query result to consume, straight to finish_sample (fsp is 0)
   } else if (!(L.fl & LF_SHADOW)) {
-    if (!hit) {  // main.cpp:351-357
-      c = cclamp(background(S, L.q.d));
+    if (!hit) {  // main.cpp:351-357 (pass 1 of a refracting frame: its colours are pass 2's)
+      c = MODE == MODE_TCHAIN ? mk(0.f, 0.f, 0.f) : cclamp(background(S, L.q.d));
     } else {
       L.hitT = L.best_t;
       L.hitPrim = L.best_prim;
@@ -1648,7 +1661,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       L.acc = mk(0, 0, 0);
       L.lightPos = mk(0, 0, 0);
       L.j = 0;
-      if (S.n_lights > 0) {
+      if (MODE != MODE_TCHAIN && S.n_lights > 0) {  // (pass 1 of a refracting frame: no shadow rays)
         setup_shadow<STATS, ACC, MODE>(S, F, L, C);
         return;
       }
@@ -1878,13 +1891,13 @@ __device__ void chain_process(const SceneArgs& S, const FrameArgs& F, Lane& L, C
 template <bool STATS, int MODE, int ACC>
 __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L, Counters& C) {
   // MODE_REPLAY lanes hold a sample slot (pixel * nsub + sample), the others a pixel
-  const uint32_t pixel = kReplay<MODE> ? L.item / (uint32_t)F.nsub : L.item;
+  const uint32_t pixel = kReadBack<MODE> ? L.item / (uint32_t)F.nsub : L.item;
   const Item it = decode_item(F, S.res_x, S.res_y, pixel, 1);
   L.depth = 1;
   L.fsp = 0;
   L.ior1 = 1.0f;
   L.fl = 0u;
-  if (STATS && !kReplay<MODE>) C.v[ST_SAMPLES]++;  // pass 1 counts the two-pass frame's samples
+  if (STATS && !kReadBack<MODE>) C.v[ST_SAMPLES]++;  // pass 1 counts the two-pass frame's samples
   if (MODE == MODE_SKEL) F.skel_rk[(size_t)L.item * F.nsub + L.smp] = L.rk;
   RayP r;
   if (F.spp > 0) {
@@ -1892,7 +1905,7 @@ __device__ void seq_start_sample(const SceneArgs& S, const FrameArgs& F, Lane& L
     const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + L.smp] : shuffle_source(F, L.pmix, (int)L.smp);
     sample_prologue_at(F, L.pmix, (int)L.smp, pos, rx, ry, sx, sy);
     const float px = (float)it.x + rx, py = (float)it.y + ry;
-    if (MODE != MODE_AREPLAY && F.dof) {  // (an AA frame's replay has no DoF: those frames are in-order)
+    if (MODE != MODE_AREPLAY && MODE != MODE_TREPLAY && F.dof) {  // (an AA frame's replay has no DoF: those frames are in-order)
       KRng rng{F.seed, L.pmix, L.rk};
       r = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
       L.rk = rng.k;
@@ -1941,7 +1954,7 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     seq_begin<STATS, MODE, ACC>(S, F, L, item, 0u, seq_first_rk(F), C);
     return;
   }
-  if (kReplay<MODE>) {  // work item = sample slot: the sample from its recorded stream position
+  if (kReadBack<MODE>) {  // work item = sample slot: the sample from its recorded stream position
     const Item it = decode_item(F, S.res_x, S.res_y, item, F.nsub);
     if (!it.valid) {  // padding of a partial tile
       F.samples[item] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1952,8 +1965,8 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     L.smp = (uint32_t)it.sub;
     // an AA / Whitted frame's replay has no stream positions (no draw after the prologue reaches the
     // frame, Q16): its rk holds the sample's closest-chain record instead (closest_query)
-    L.rk = MODE == MODE_REPLAY ? F.skel_rk[item]
-                               : (F.chain_div > 1 ? ((uint32_t)item - (uint32_t)it.sub) / (uint32_t)F.chain_div : item);
+    const uint32_t rec = F.chain_div > 1 ? ((uint32_t)item - (uint32_t)it.sub) / (uint32_t)F.chain_div : item;
+    L.rk = MODE == MODE_REPLAY ? F.skel_rk[item] : (MODE == MODE_TREPLAY ? rec * (uint32_t)F.tree_recs : rec);
     seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
     return;
   }
@@ -1988,9 +2001,10 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
   L.fsp = 0;
   L.ior1 = 1.0f;
   L.fl = 0u;
-  if (STATS) C.v[ST_SAMPLES] += MODE == MODE_CHAIN ? (uint32_t)F.chain_div : 1u;
+  if (STATS) C.v[ST_SAMPLES] += (MODE == MODE_CHAIN || MODE == MODE_TCHAIN) ? (uint32_t)F.chain_div : 1u;
+  if (MODE == MODE_TCHAIN) L.rk = item * (uint32_t)F.tree_recs;  // the sample's first hit record
   RayP r;
-  if (MODE == MODE_AA || (MODE == MODE_CHAIN && F.spp > 0)) {
+  if (MODE == MODE_AA || ((MODE == MODE_CHAIN || MODE == MODE_TCHAIN) && F.spp > 0)) {
     const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     float rx, ry, sx, sy;
     const int pos = F.perm ? (int)F.perm[item] : shuffle_source(F, pmix, it.sub);  // item = pixel * spp + sub
@@ -2172,7 +2186,8 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
 #else
         constexpr int kLeaf1 =
-            !TRI_ONLY || kReplay<MODE> || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
+            !TRI_ONLY || kReadBack<MODE> || MODE == MODE_SEQ ? 0
+                                                             : (MODE == MODE_SKEL || MODE == MODE_CHAIN || MODE == MODE_TCHAIN ? 1 : 2);
 #endif
         // The shadow tree stays out of the path kernel (measured, round 4, headline 512^2 x 64 spp): its
         // lanes walked 26 % fewer node records per ray (75.8 -> 56.2 visits), but a wave whose lanes
@@ -2533,6 +2548,8 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
     case MODE_SKEL: launch_persistent_m<T, ST, MODE_SKEL, A>(S, F, st); break;
     case MODE_REPLAY: launch_persistent_m<T, ST, MODE_REPLAY, A>(S, F, st); break;
     case MODE_AREPLAY: launch_persistent_m<T, ST, MODE_AREPLAY, A>(S, F, st); break;
+    case MODE_TCHAIN: launch_persistent_m<T, ST, MODE_TCHAIN, A>(S, F, st); break;
+    case MODE_TREPLAY: launch_persistent_m<T, ST, MODE_TREPLAY, A>(S, F, st); break;
     case MODE_CHAIN: launch_persistent_m<T, ST, MODE_CHAIN, A>(S, F, st); break;
     case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG, A>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT, A>(S, F, st); break;

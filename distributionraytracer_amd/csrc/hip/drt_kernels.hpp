@@ -27,9 +27,15 @@ enum FrameMode : int {
   MODE_CHAIN = 7,   // pass 1, one lane per (pixel, sample): the sample's closest-hit chain only,
                     // each bounce's hit recorded; pass 2 is MODE_REPLAY.  A Whitted frame (spp 0,
                     // round 5) in two passes: one lane per pixel, the chain its light samples share
-  MODE_AREPLAY = 8  // pass 2 of an AA / Whitted frame (round 5: its own instantiation; MODE_REPLAY
+  MODE_AREPLAY = 8,  // pass 2 of an AA / Whitted frame (round 5: its own instantiation; MODE_REPLAY
                     // stays the in-order frames'): no keyed-stream draw after the prologue reaches
                     // the frame, so no RNG, DoF or stream positions in its code
+  // An AA / Whitted frame of a scene WITH a refracting material in two passes (round 5): a sample's
+  // closest hits form a binary tree (refraction child first, then reflection, main.cpp:465-512):
+  MODE_TCHAIN = 9,   // pass 1: the whole tree of closest-hit queries, no shadow rays, each hit recorded
+                     // in the order rayTracing() makes the queries (<= 2^(max_depth+1) - 1 per sample)
+  MODE_TREPLAY = 10  // pass 2: the whole rayTracing() with refraction, the closest hits read back in
+                     // that order, shadow queries on the shadow tree / the Grid
 };
 
 enum StatSlot : int {
@@ -171,6 +177,9 @@ struct FrameArgs {
   // replay passes: frame heads, max_depth + 1 float4 per resident lane (blockIdx * blockDim +
   // threadIdx), each lane's run contiguous
   float4* heads;
+  // MODE_TCHAIN / MODE_TREPLAY: records per sample (2^(max_depth+1) - 1); a lane's rk holds its next
+  // record index
+  int tree_recs;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

@@ -934,3 +934,39 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
     monkeypatch.delenv("DRT_WHITTED_TWO_PASS")
     monkeypatch.setenv("DRT_AA_TWO_PASS", "1")
     assert renderer.plan(renderer.frame_params(seed=4, **kw))["passes"] == (2 if first == "quad" else 1)
+
+
+@pytest.mark.parametrize("accel,spp", [("bvh", 4), ("grid", 4), ("bvh", 0), ("grid", 0)])
+def test_refraction_two_pass_frame_equals_one_pass(drt, oracle_mod, renderer, tmp_path, monkeypatch, accel, spp):
+    """AA and Whitted frames of scenes WITH a refracting material (glass spheres, trans 1) run in two
+    passes (round 5; FrameMode MODE_TCHAIN / MODE_TREPLAY): a sample's closest hits form a binary tree
+    (refraction child first, then reflection, main.cpp:465-512); pass 1 records the whole tree in
+    rayTracing()'s query order without shadow rays, pass 2 runs rayTracing() with the hits read back in
+    that order.  The frame equals the one-pass frame (DRT_TREE_TWO_PASS=0), the reference-order frame
+    and the oracle; samples and shadow rays are equal, closest-hit work equal (AA) or grid_res times
+    smaller (the Whitted light samples of a pixel share its tree)."""
+    text = sg.mixed_scene_text(res=(40, 32), spp=spp, accel=accel, n_tris=1500)
+    s, o = load_both(drt, oracle_mod, tmp_path, text)
+    s.build()
+    renderer.upload(s)
+    kw = {"max_depth": 5}
+    assert renderer.plan(renderer.frame_params(seed=9, **kw))["passes"] == 2
+    img = renderer.render(seed=9, stats=True, **kw)
+    st = renderer.stats()
+    monkeypatch.setenv("DRT_TREE_TWO_PASS", "0")
+    assert renderer.plan(renderer.frame_params(seed=9, **kw))["passes"] == 1
+    one = renderer.render(seed=9, stats=True, **kw)
+    st1 = renderer.stats()
+    ref = renderer.render(seed=9, stats=True, reference_order=True, **kw)
+    rst = renderer.stats()
+    np.testing.assert_array_equal(bits(img), bits(one))
+    np.testing.assert_array_equal(bits(img), bits(ref))
+    oimg, ost = o.render(seed=9, **kw)
+    compare_images(img, oimg)
+    div = 4 if spp == 0 else 1  # mixed_scene_text's quad light 0 has gridRes 4
+    assert st["samples"] == st1["samples"] == rst["samples"]
+    assert st["shadow_rays"] == st1["shadow_rays"] == rst["shadow_rays"]
+    for k in ("closest_rays", "closest_inner", "closest_leaf", "closest_prims"):
+        assert st1[k] == rst[k], k
+        assert st[k] * div == st1[k], k
+    assert st1["closest_rays"] == ost["closest_calls"] and st1["shadow_rays"] == ost["shadow_calls"]
