@@ -326,6 +326,48 @@ __device__ __forceinline__ V3 light_term(const drt_material& m, float NdotL, flo
   if (F.light_spp > 1 && Lt.type == DRT_LIGHT_QUAD) c = mul(c, F.light_inv);
   return c;
 }
+// Material / light table reads of the persistent kernels' shading.  -DDRT_UNIFORM_TABLES (A/B): when
+// the active lanes of the wave read at most two distinct entries (one material and the two lights of
+// the benchmark scenes), the entries come through scalar loads (SMEM, the scalar cache) and a per-lane
+// select instead of per-lane vector loads on the vector-memory path the kernel is bound by.
+#ifdef DRT_UNIFORM_TABLES
+template <class T>
+__device__ __forceinline__ T tab(const T* base, uint32_t i) {
+  typedef const __attribute__((address_space(4))) uint32_t CU;
+  constexpr int N = (int)(sizeof(T) / 4);
+  static_assert(sizeof(T) % 4 == 0, "dword table entries");
+  const uint32_t i0 = __builtin_amdgcn_readfirstlane(i);
+  const uint64_t other = __ballot(i != i0);
+  T r;
+  if (other == 0) {
+    CU* p = (CU*)(const void*)(base + i0);
+    uint32_t w[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) w[k] = p[k];
+    __builtin_memcpy(&r, w, sizeof(T));
+  } else {
+    const uint32_t i1 = __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(other));
+    if (__ballot(i != i0 && i != i1) == 0) {
+      CU* p0 = (CU*)(const void*)(base + i0);
+      CU* p1 = (CU*)(const void*)(base + i1);
+      const bool second = i == i1;
+      uint32_t w[N];
+#pragma unroll
+      for (int k = 0; k < N; k++) w[k] = second ? p1[k] : p0[k];
+      __builtin_memcpy(&r, w, sizeof(T));
+    } else {
+      r = base[i];
+    }
+  }
+  return r;
+}
+#else
+template <class T>
+__device__ __forceinline__ const T& tab(const T* base, uint32_t i) {
+  return base[i];
+}
+#endif
+
 // Light index of pair j (no integer division in the reference case m = 1).
 __device__ __forceinline__ int light_of_pair(int j, const FrameArgs& F) {
   return F.light_spp == 1 ? j : j / F.light_spp;
@@ -1489,7 +1531,7 @@ template <bool STATS, int ACC, int MODE>
 __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs& F, Lane& L,
                                              Counters& C) {  // main.cpp:386-422
   const int li = light_of_pair(L.j, F);
-  L.lightPos = light_point(S.lights[li], L.ls, L.j - li * F.light_spp, F);
+  L.lightPos = light_point(tab(S.lights, (uint32_t)li), L.ls, L.j - li * F.light_spp, F);
   V3 Lv = sub(L.lightPos, L.hitP);
   const V3 Ls = Lv;
   Lv = normalize(Lv);
@@ -1668,7 +1710,8 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       after_lights = true;
     }
   } else {  // main.cpp:444-450
-    if (!hit) L.acc = add(L.acc, light_term(S.mats[L.mat], L.NdotL, L.NdotH, S.lights[light_of_pair(L.j, F)], F));
+    if (!hit)
+      L.acc = add(L.acc, light_term(tab(S.mats, L.mat), L.NdotL, L.NdotH, tab(S.lights, (uint32_t)light_of_pair(L.j, F)), F));
     L.j = next_light_pair(S, F, L.j);
     if (L.j < S.n_lights * F.light_spp) {
       setup_shadow<STATS, ACC, MODE>(S, F, L, C);
@@ -1677,7 +1720,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
     after_lights = true;
   }
   if (after_lights) {  // main.cpp:453-520
-    const drt_material& m = S.mats[L.mat];
+    const drt_material& m = tab(S.mats, L.mat);
     const bool outside = (L.fl & LF_OUTSIDE) != 0u;
     if (L.depth > F.max_depth) {
       c = L.acc;
@@ -1765,8 +1808,9 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       const uint32_t w = __float_as_uint(h.w), flags = w >> 24, mat = w & 0xffffffu;
       V3 acc = mk(h.x, h.y, h.z);
       if (flags & 8u) {
-        const float kr = (flags & 16u) ? 1.0f : S.mats[mat].refl;
-        acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(S.mats[mat].spec)));
+        const drt_material& mm = tab(S.mats, mat);
+        const float kr = (flags & 16u) ? 1.0f : mm.refl;
+        acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(mm.spec)));
       }
       c = cclamp(acc);
       L.fsp--;
@@ -1795,7 +1839,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
         L.fsp--;
       } else {
         const V3 rc = cclamp(c);
-        if (f.flags & 8u) f.acc = add(f.acc, cmulc(mul(rc, f.kr), ld3(S.mats[f.mat].spec)));
+        if (f.flags & 8u) f.acc = add(f.acc, cmulc(mul(rc, f.kr), ld3(tab(S.mats, f.mat).spec)));
         c = cclamp(f.acc);
         L.fsp--;
       }
@@ -1822,7 +1866,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
         return;
       }
     } else if (flags & 8u) {  // reflection child returned, reflectDir.N > 0 (main.cpp:513-518)
-      acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(S.mats[f.mat].spec)));
+      acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(tab(S.mats, f.mat).spec)));
     }
     c = cclamp(acc);
     L.fsp--;
@@ -1843,7 +1887,7 @@ __device__ void skel_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Co
       make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
   if (hit && L.depth <= F.max_depth) {
     const uint32_t mat = prim_material(S.prims[3 * L.best_prim]);
-    if (S.mats[mat].ks > 0.0f) {
+    if (tab(S.mats, mat).ks > 0.0f) {
       const V3 hitP = add(L.q.o, mul(L.q.d, L.best_t));  // main.cpp:361
       V3 N = normalize(prim_normal(S.prims, L.best_prim, L.q, L.best_t));
       if (!(dot(L.q.d, N) < 0.0f)) N = neg(N);
@@ -1871,7 +1915,7 @@ __device__ void chain_process(const SceneArgs& S, const FrameArgs& F, Lane& L, C
       make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
   if (hit && L.depth <= F.max_depth) {
     const uint32_t mat = prim_material(S.prims[3 * L.best_prim]);
-    if (S.mats[mat].ks > 0.0f) {
+    if (tab(S.mats, mat).ks > 0.0f) {
       const V3 hitP = add(L.q.o, mul(L.q.d, L.best_t));  // main.cpp:361
       V3 N = normalize(prim_normal(S.prims, L.best_prim, L.q, L.best_t));
       if (!(dot(L.q.d, N) < 0.0f)) N = neg(N);

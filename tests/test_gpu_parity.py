@@ -970,3 +970,30 @@ def test_refraction_two_pass_frame_equals_one_pass(drt, oracle_mod, renderer, tm
         assert st1[k] == rst[k], k
         assert st[k] * div == st1[k], k
     assert st1["closest_rays"] == ost["closest_calls"] and st1["shadow_rays"] == ost["shadow_calls"]
+
+
+def test_frame_pass_times_split_the_path_time(drt, monkeypatch):
+    """drt_frame_pass_times (round 5; bench.py roofline.passes): a two-pass frame's closest-chain and
+    replay launches, timed on the frame's stream, add up to its path-kernel time; a one-pass frame
+    reports its kernel as pass 1 and 0 for pass 2."""
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(20_000), 96, 16)
+    s.build()
+    r = drt.Renderer(0)
+    try:
+        r.upload(s)
+        monkeypatch.setenv("DRT_AA_TWO_PASS", "2")
+        for _ in range(3):
+            r.render(seed=5)
+        monkeypatch.setenv("DRT_AA_TWO_PASS", "0")
+        for _ in range(3):
+            r.render(seed=5)
+        path_ms, _ = r.frame_times(6)
+        p1, p2 = r.frame_pass_times(6)
+        assert len(p1) == len(p2) == 6
+        assert (p1 > 0).all() and (p2[:3] > 0).all() and (p2[3:] == 0).all()
+        np.testing.assert_allclose(p1 + p2, path_ms, rtol=1e-3, atol=2e-3)
+    finally:
+        r.close()

@@ -35,6 +35,10 @@ SCENE_CASES = {
     "assignment1_grid_whitted_sky": ("assignment1", {}, {}),
     "dragon_assignment1_bvh_whitted_sky": ("dragon_assignment1", {}, {}),
     "dragon_assignment1_bvh_aa16": ("dragon_assignment1", dict(res=(256, 256), spp=16), {}),
+    # round 5: AA frames of scenes with glass (trans 1) run as MODE_TCHAIN + MODE_TREPLAY two-pass frames
+    # in this suite (DRT_AA_TWO_PASS=2, tests/conftest.py)
+    "balls_high_bvh_aa16_glass": ("balls_high", dict(accel="bvh", res=(192, 192), spp=16), {}),
+    "assignment1_grid_aa4_glass": ("assignment1", dict(res=(128, 128), spp=4), {}),
 }
 
 
