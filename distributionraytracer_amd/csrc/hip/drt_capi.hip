@@ -24,6 +24,8 @@ void launch_path_persistent(const SceneArgs& S, const FrameArgs& F, int accel, b
 void launch_trace_stream(const SceneArgs& S, const TraceArgs& A, bool shadow, bool tri_only, bool stats, int waves,
                          hipStream_t st);
 void launch_trace_prep(const float* rays, int n, int shadow, float4* out, hipStream_t st);
+void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
+void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
 void launch_trace_finish(const SceneArgs& S, const float4* q, int n, float* t, const uint32_t* prim, float* nrm,
                          int32_t* obj, hipStream_t st);
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
@@ -108,6 +110,8 @@ struct drt_ctx {
   // two-pass in-order frames: per sample slot its stream position, per slot and bounce its closest hit
   DevBuf d_skel_rk_s[DRT_FRAME_SLOTS], d_skel_hits_s[DRT_FRAME_SLOTS];
   DevBuf d_heads_s[DRT_FRAME_SLOTS];  // replay passes: frame heads, max_depth + 1 per resident lane
+  // wavefront replay (WfArgs): shadow queries, their Phong factors and answers, per-level records
+  DevBuf d_wf_rays_s[DRT_FRAME_SLOTS], d_wf_nl_s[DRT_FRAME_SLOTS], d_wf_occ_s[DRT_FRAME_SLOTS], d_wf_lvl_s[DRT_FRAME_SLOTS];
   int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
@@ -1250,6 +1254,32 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());
     DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
+    // Pass 2 of an AA / Whitted BVH frame without refraction as a wavefront (round 5, WfArgs): every
+    // shadow query of the frame generated from the recorded chains, answered by the streaming kernel,
+    // combined per sample.  DRT_WAVEFRONT=0 keeps the persistent MODE_AREPLAY pass; a frame whose query
+    // array does not fit (2^32 query slots, device memory) keeps it too.  Both render the same frame.
+    bool wavefront = false;
+    WfArgs W{};
+    if (P.aa_chain && !P.tree && c->accel == DRT_ACCEL_BVH && c->has_wide && env_int("DRT_WAVEFRONT", 1) != 0) {
+      const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = (uint64_t)c->lights.size() * (uint64_t)P.F.light_spp;
+      const uint64_t q = levels * pairs * P.n_slots;
+      if (P.n_slots < 0xFFFFFFFFull && q < 0xFFFFFF00ull &&
+          c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.n_slots) == hipSuccess) {
+        wavefront = true;
+        W.rays = c->d_wf_rays_s[slot].as<float4>();
+        W.nl = c->d_wf_nl_s[slot].as<float2>();
+        W.occ = c->d_wf_occ_s[slot].as<uint8_t>();
+        W.lvl = c->d_wf_lvl_s[slot].as<float4>();
+        W.n_slots = (uint32_t)P.n_slots;
+        W.pairs = (int)pairs;
+      } else {
+        (void)hipGetLastError();
+        for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot]}) b->release();
+      }
+    }
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
     F2.mode = P.tree ? MODE_TREPLAY : (P.aa_chain ? MODE_AREPLAY : MODE_REPLAY);
     F2.heads = (!P.aa_chain && c->accel == DRT_ACCEL_BVH) ? c->d_heads_s[slot].as<float4>() : nullptr;
@@ -1262,7 +1292,26 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     F2.work_counter = d_counter.as<unsigned int>() + 256;
-    launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
+    if (wavefront) {
+      launch_wf_gen(S, F2, W, st);
+      DRT_HIP(c, hipGetLastError());
+      const uint64_t q = (uint64_t)(P.F.max_depth + 1) * (uint64_t)W.pairs * W.n_slots;
+      if (q) {
+        TraceArgs A{};
+        A.rays = W.rays;
+        A.n = (uint32_t)q;
+        A.counter = F2.work_counter;
+        A.occ_out = W.occ;
+        A.stats = F2.stats;
+        A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 24);
+        A.sparse = 1;
+        launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 6), st);
+        DRT_HIP(c, hipGetLastError());
+      }
+      launch_wf_combine(S, F2, W, st);
+    } else {
+      launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
+    }
   } else if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
     else launch_path(S, P.F, c->accel, c->tri_only, stats, st);

@@ -326,13 +326,16 @@ __device__ __forceinline__ V3 light_term(const drt_material& m, float NdotL, flo
   if (F.light_spp > 1 && Lt.type == DRT_LIGHT_QUAD) c = mul(c, F.light_inv);
   return c;
 }
-// Material / light table reads of the persistent kernels' shading.  -DDRT_UNIFORM_TABLES (A/B): when
+// Material / light table reads of the persistent kernels' shading (round 5).  In the BVH kernels, when
 // the active lanes of the wave read at most two distinct entries (one material and the two lights of
 // the benchmark scenes), the entries come through scalar loads (SMEM, the scalar cache) and a per-lane
-// select instead of per-lane vector loads on the vector-memory path the kernel is bound by.
-#ifdef DRT_UNIFORM_TABLES
-template <class T>
-__device__ __forceinline__ T tab(const T* base, uint32_t i) {
+// select instead of per-lane vector loads on the vector-memory path the kernel is bound by: replay
+// vector-memory read instructions 843 -> 822 M per headline frame (scalar 377 -> 468 M), headline
+// +0.3 %, C3 +0.2 %, C4 +1.9 %; the Grid stepper measured 2.8 % slower with it (register allocation)
+// and keeps per-lane loads (profiles/r05_ab_uniform_tables_chain_leaf.jsonl).  -DDRT_NO_UNIFORM_TABLES
+// turns it off (A/B).
+template <bool UNI, class T>
+__device__ __forceinline__ T tab_uni(const T* base, uint32_t i) {
   typedef const __attribute__((address_space(4))) uint32_t CU;
   constexpr int N = (int)(sizeof(T) / 4);
   static_assert(sizeof(T) % 4 == 0, "dword table entries");
@@ -361,12 +364,13 @@ __device__ __forceinline__ T tab(const T* base, uint32_t i) {
   }
   return r;
 }
-#else
-template <class T>
-__device__ __forceinline__ const T& tab(const T* base, uint32_t i) {
+template <int ACC, class T>
+__device__ __forceinline__ T tab(const T* base, uint32_t i) {
+#ifndef DRT_NO_UNIFORM_TABLES
+  if constexpr (ACC == ACC_BVH) return tab_uni<true>(base, i);
+#endif
   return base[i];
 }
-#endif
 
 // Light index of pair j (no integer division in the reference case m = 1).
 __device__ __forceinline__ int light_of_pair(int j, const FrameArgs& F) {
@@ -1531,7 +1535,7 @@ template <bool STATS, int ACC, int MODE>
 __device__ __forceinline__ void setup_shadow(const SceneArgs& S, const FrameArgs& F, Lane& L,
                                              Counters& C) {  // main.cpp:386-422
   const int li = light_of_pair(L.j, F);
-  L.lightPos = light_point(tab(S.lights, (uint32_t)li), L.ls, L.j - li * F.light_spp, F);
+  L.lightPos = light_point(tab<ACC>(S.lights, (uint32_t)li), L.ls, L.j - li * F.light_spp, F);
   V3 Lv = sub(L.lightPos, L.hitP);
   const V3 Ls = Lv;
   Lv = normalize(Lv);
@@ -1711,7 +1715,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
     }
   } else {  // main.cpp:444-450
     if (!hit)
-      L.acc = add(L.acc, light_term(tab(S.mats, L.mat), L.NdotL, L.NdotH, tab(S.lights, (uint32_t)light_of_pair(L.j, F)), F));
+      L.acc = add(L.acc, light_term(tab<ACC>(S.mats, L.mat), L.NdotL, L.NdotH, tab<ACC>(S.lights, (uint32_t)light_of_pair(L.j, F)), F));
     L.j = next_light_pair(S, F, L.j);
     if (L.j < S.n_lights * F.light_spp) {
       setup_shadow<STATS, ACC, MODE>(S, F, L, C);
@@ -1720,7 +1724,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
     after_lights = true;
   }
   if (after_lights) {  // main.cpp:453-520
-    const drt_material& m = tab(S.mats, L.mat);
+    const drt_material& m = tab<ACC>(S.mats, L.mat);
     const bool outside = (L.fl & LF_OUTSIDE) != 0u;
     if (L.depth > F.max_depth) {
       c = L.acc;
@@ -1808,7 +1812,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
       const uint32_t w = __float_as_uint(h.w), flags = w >> 24, mat = w & 0xffffffu;
       V3 acc = mk(h.x, h.y, h.z);
       if (flags & 8u) {
-        const drt_material& mm = tab(S.mats, mat);
+        const drt_material& mm = tab<ACC>(S.mats, mat);
         const float kr = (flags & 16u) ? 1.0f : mm.refl;
         acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(mm.spec)));
       }
@@ -1839,7 +1843,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
         L.fsp--;
       } else {
         const V3 rc = cclamp(c);
-        if (f.flags & 8u) f.acc = add(f.acc, cmulc(mul(rc, f.kr), ld3(tab(S.mats, f.mat).spec)));
+        if (f.flags & 8u) f.acc = add(f.acc, cmulc(mul(rc, f.kr), ld3(tab<ACC>(S.mats, f.mat).spec)));
         c = cclamp(f.acc);
         L.fsp--;
       }
@@ -1866,7 +1870,7 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
         return;
       }
     } else if (flags & 8u) {  // reflection child returned, reflectDir.N > 0 (main.cpp:513-518)
-      acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(tab(S.mats, f.mat).spec)));
+      acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(tab<ACC>(S.mats, f.mat).spec)));
     }
     c = cclamp(acc);
     L.fsp--;
@@ -1887,7 +1891,7 @@ __device__ void skel_process(const SceneArgs& S, const FrameArgs& F, Lane& L, Co
       make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
   if (hit && L.depth <= F.max_depth) {
     const uint32_t mat = prim_material(S.prims[3 * L.best_prim]);
-    if (tab(S.mats, mat).ks > 0.0f) {
+    if (tab<ACC>(S.mats, mat).ks > 0.0f) {
       const V3 hitP = add(L.q.o, mul(L.q.d, L.best_t));  // main.cpp:361
       V3 N = normalize(prim_normal(S.prims, L.best_prim, L.q, L.best_t));
       if (!(dot(L.q.d, N) < 0.0f)) N = neg(N);
@@ -1915,7 +1919,7 @@ __device__ void chain_process(const SceneArgs& S, const FrameArgs& F, Lane& L, C
       make_uint2(__float_as_uint(L.best_t), hit ? L.best_prim : 0xFFFFFFFFu);
   if (hit && L.depth <= F.max_depth) {
     const uint32_t mat = prim_material(S.prims[3 * L.best_prim]);
-    if (tab(S.mats, mat).ks > 0.0f) {
+    if (tab<ACC>(S.mats, mat).ks > 0.0f) {
       const V3 hitP = add(L.q.o, mul(L.q.d, L.best_t));  // main.cpp:361
       V3 N = normalize(prim_normal(S.prims, L.best_prim, L.q, L.best_t));
       if (!(dot(L.q.d, N) < 0.0f)) N = neg(N);
@@ -2229,9 +2233,14 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
 #ifdef DRT_REPLAY_LEAF1  // (A/B) one primitive per step in the replay pass too
         constexpr int kLeaf1 = !TRI_ONLY || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_CHAIN ? 1 : 2);
 #else
+#ifdef DRT_CHAIN_LEAF1_2  // (A/B) the AA closest-chain pass leaves a one-primitive leaf step's last slot unread
+        constexpr int kLeaf1 =
+            !TRI_ONLY || kReadBack<MODE> || MODE == MODE_SEQ ? 0 : (MODE == MODE_SKEL || MODE == MODE_TCHAIN ? 1 : 2);
+#else
         constexpr int kLeaf1 =
             !TRI_ONLY || kReadBack<MODE> || MODE == MODE_SEQ ? 0
                                                              : (MODE == MODE_SKEL || MODE == MODE_CHAIN || MODE == MODE_TCHAIN ? 1 : 2);
+#endif
 #endif
         // The shadow tree stays out of the path kernel (measured, round 4, headline 512^2 x 64 spp): its
         // lanes walked 26 % fewer node records per ray (75.8 -> 56.2 visits), but a wave whose lanes
@@ -2325,6 +2334,11 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
     const uint64_t idle = __ballot(L.item == kNoItem);
     const int n_idle = __popcll(idle);
     if (n_idle >= A.refill_min || n_idle == 64) {
+      // a sparse query array (A.sparse: the wavefront replay's, thr < 0 = no query in the slot) is
+      // walked until the idle lanes hold queries or fewer than refill_min lanes are left idle
+      uint64_t want = idle;
+      int n_want = n_idle;
+      while (true) {
       if (chunk_next >= chunk_end && !exhausted) {
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(A.counter, kTraceChunk);
@@ -2334,10 +2348,12 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
         if (base + kTraceChunk >= A.n) exhausted = true;
       }
       if (L.item == kNoItem) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
         const uint32_t it = chunk_next + rank;
         if (it < chunk_end) {
-          const float4 a = A.rays[2 * (size_t)it], b = A.rays[2 * (size_t)it + 1];
+          const float4 a = A.rays[2 * (size_t)it];
+          if (!A.sparse || a.w >= 0.0f) {
+          const float4 b = A.rays[2 * (size_t)it + 1];
           L.item = it;
           L.q = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
           L.thr = a.w;
@@ -2356,9 +2372,15 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
             L.fl |= LF_WIDE;
             L.cur = S.wroot;
           }
+          }
         }
       }
-      chunk_next = min(chunk_next + (uint32_t)n_idle, chunk_end);
+      chunk_next = min(chunk_next + (uint32_t)n_want, chunk_end);
+      if (!A.sparse) break;
+      want = __ballot(L.item == kNoItem);
+      n_want = __popcll(want);
+      if (n_want < A.refill_min || (exhausted && chunk_next >= chunk_end)) break;
+      }
     }
     const bool in_trav = L.item != kNoItem && (L.fl & LF_TRAV);
     const uint64_t trav = __ballot(in_trav);
@@ -2391,6 +2413,170 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
       if (lane == 0 && v) atomicAdd(&A.stats[s], v);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Wavefront replay (round 5; drt_kernels.hpp WfArgs): an AA / Whitted two-pass BVH frame without
+// refraction, pass 2 as three launches — wf_gen, trace_stream over every shadow query of the frame,
+// wf_combine — instead of the persistent MODE_AREPLAY kernel, whose waves interleave shading (a third
+// of their lanes active) with the shadow traversal.  The arithmetic is lane_process's, in its order:
+// setup_shadow's light point, ray and Phong factors per (level, light pair), the unshadowed terms added
+// in pair order, the depth cut, and the mirror unwind.
+// ------------------------------------------------------------------------------------------
+enum : uint32_t { WF_MISS = 1u, WF_DEEP = 2u, WF_REFL = 4u, WF_RN = 8u, WF_KR1 = 16u };
+
+__device__ __forceinline__ bool wf_pair_used(const SceneArgs& S, const FrameArgs& F, int j) {
+  // the pairs next_light_pair visits: every quad-light pair, a point light's k = 0 only
+  const int m = F.light_spp;
+  return m == 1 || j % m == 0 || S.lights[j / m].type == DRT_LIGHT_QUAD;
+}
+
+__global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= W.n_slots) return;
+  const size_t ns = W.n_slots;
+  const int md = F.max_depth, np = W.pairs;
+  const Item it = decode_item(F, S.res_x, S.res_y, slot, F.nsub);
+  int l = 0;
+  if (it.valid) {
+    const uint32_t rec = F.chain_div > 1 ? (slot - (uint32_t)it.sub) / (uint32_t)F.chain_div : slot;
+    // the sample's primary ray and light sample (seq_start_sample, MODE_AREPLAY)
+    RayP q;
+    V3 ls;
+    if (F.spp > 0) {
+      const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+      const uint32_t pixel = slot / (uint32_t)F.nsub;
+      float rx, ry, sx, sy;
+      const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + it.sub] : shuffle_source(F, pmix, it.sub);
+      sample_prologue_at(F, pmix, it.sub, pos, rx, ry, sx, sy);
+      q = primary_ray(S, (float)it.x + rx, (float)it.y + ry);
+      ls = mk(sx, sy, 0.0f);
+    } else {
+      const int sb = it.sub;
+      q = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
+      ls = F.grid_res ? mk(((float)(sb % F.grid_size) + 0.5f) / (float)F.grid_size,
+                           ((float)(sb / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
+                      : mk(0.5f, 0.5f, 0.0f);
+    }
+    for (; l <= md; l++) {
+      const uint2 h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)l];
+      const size_t li_ = (size_t)l * ns + slot;
+      if (h.y == 0xFFFFFFFFu) {  // main.cpp:351-357
+        const V3 c = cclamp(background(S, q.d));
+        W.lvl[li_] = make_float4(c.x, c.y, c.z, __uint_as_float(WF_MISS << 24));
+        break;
+      }
+      const float t = __uint_as_float(h.x);
+      const uint32_t prim = h.y;
+      const V3 hitP = add(q.o, mul(q.d, t));
+      V3 N = normalize(prim_normal(S.prims, prim, q, t));
+      const bool outside = dot(q.d, N) < 0.0f;
+      if (!outside) N = neg(N);
+      const uint32_t mat = prim_material(S.prims[3 * prim]);
+      const V3 V = neg(normalize(q.d));
+      V3 lightPos = mk(0, 0, 0);
+      for (int j = 0; j < np; j++) {  // setup_shadow for every pair the light loop visits
+        const size_t qi = ((size_t)l * np + j) * ns + slot;
+        if (!wf_pair_used(S, F, j)) {
+          W.rays[2 * qi] = make_float4(0.f, 0.f, 0.f, -1.0f);
+          continue;
+        }
+        const int li = light_of_pair(j, F);
+        lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
+        V3 Lv = sub(lightPos, hitP);
+        const V3 Ls = Lv;
+        Lv = normalize(Lv);
+        const V3 H = normalize(add(Lv, V));
+        const float NdotL = smax(dot(N, Lv), 0.0f), NdotH = smax(dot(N, H), 0.0f);
+        const V3 so = add(hitP, mul(N, 1e-4f));
+        const V3 sd = normalize(Ls);
+        W.rays[2 * qi] = make_float4(so.x, so.y, so.z, shadow_threshold(length(Ls)));
+        W.rays[2 * qi + 1] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+        W.nl[qi] = make_float2(NdotL, NdotH);
+      }
+      uint32_t flags = 0u;
+      bool more = false;
+      if (l + 1 > md) {  // depth > MAX_DEPTH: the accumulated colour, unclamped (main.cpp:454)
+        flags = WF_DEEP;
+      } else {
+        const drt_material m = S.mats[mat];
+        float kr = m.refl;
+        float ior2 = m.ior;
+        if (!outside) ior2 = 1.0f;
+        const float eta = 1.0f / ior2;  // ior1: mirror children keep the camera's 1.0
+        const V3 Vt = sub(mul(N, dot(V, N)), V);
+        const float sin_t = eta * length(Vt);
+        if (m.trans > 0.0f && sin_t >= 1.0f) kr = 1.0f;  // (trans == 1 never reaches a two-pass frame)
+        if (m.ks > 0.0f) {
+          const V3 R = normalize(sub(mul(mul(N, dot(V, N)), 2.0f), V));
+          flags = WF_REFL | (dot(R, N) > 0.0f ? WF_RN : 0u) | (kr == 1.0f && m.refl != 1.0f ? WF_KR1 : 0u);
+          q = make_ray(add(hitP, mul(N, 1e-4f)), R);
+          ls = lightPos;
+          more = true;
+        }
+      }
+      W.lvl[li_] = make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24)));
+      if (!more) {
+        l++;
+        break;
+      }
+    }
+  }
+  // no shadow query in the levels past the chain's end (a miss level has none either)
+  for (int k = it.valid ? l : 0; k <= md; k++)
+    for (int j = 0; j < np; j++) W.rays[2 * (((size_t)k * np + j) * ns + slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+}
+
+__global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= W.n_slots) return;
+  const size_t ns = W.n_slots;
+  const int md = F.max_depth, np = W.pairs;
+  const Item it = decode_item(F, S.res_x, S.res_y, slot, F.nsub);
+  if (!it.valid) {  // padding of a partial tile
+    F.samples[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  // the last level of the chain: a miss, the depth cut, or a hit without a mirror child
+  int last = 0;
+  for (; last < md; last++) {
+    const uint32_t fl = __float_as_uint(W.lvl[(size_t)last * ns + slot].w) >> 24;
+    if (!(fl & WF_REFL)) break;
+  }
+  V3 c = mk(0, 0, 0);
+  for (int l = last; l >= 0; l--) {
+    const float4 rv = W.lvl[(size_t)l * ns + slot];
+    const uint32_t w = __float_as_uint(rv.w), flags = w >> 24, mat = w & 0xffffffu;
+    if (flags & WF_MISS) {
+      c = mk(rv.x, rv.y, rv.z);
+      continue;
+    }
+    const drt_material m = S.mats[mat];
+    V3 acc = mk(0, 0, 0);
+    for (int j = 0; j < np; j++) {  // main.cpp:444-450, in the light loop's order
+      const size_t qi = ((size_t)l * np + j) * ns + slot;
+      if (!wf_pair_used(S, F, j) || W.occ[qi]) continue;
+      const float2 nl = W.nl[qi];
+      acc = add(acc, light_term(m, nl.x, nl.y, S.lights[light_of_pair(j, F)], F));
+    }
+    if (flags & WF_DEEP) {
+      c = acc;
+    } else {
+      if (flags & WF_RN) {  // the mirror child returned c (main.cpp:513-518)
+        const float kr = (flags & WF_KR1) ? 1.0f : m.refl;
+        acc = add(acc, cmulc(mul(cclamp(c), kr), ld3(m.spec)));
+      }
+      c = cclamp(acc);
+    }
+  }
+  F.samples[slot] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {
+  hipLaunchKernelGGL(wf_gen_kernel, dim3((W.n_slots + 255) / 256), dim3(256), 0, st, S, F, W);
+}
+void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {
+  hipLaunchKernelGGL(wf_combine_kernel, dim3((W.n_slots + 255) / 256), dim3(256), 0, st, S, F, W);
 }
 
 // Batched-query front end: rays n x {ox,oy,oz,dx,dy,dz} -> streaming-query records with the

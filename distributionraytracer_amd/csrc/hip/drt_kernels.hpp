@@ -187,6 +187,22 @@ struct FrameArgs {
 // 64-bit pair, and the pixels finished, on a 128-B line of its own (every pixel adds to it).
 constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 192;
 
+// Wavefront replay of an AA / Whitted two-pass BVH frame without refraction (round 5): the closest hits
+// are all known after MODE_CHAIN, so every shading decision except occlusion is a function of them.
+// wf_gen (one thread per sample slot) walks each sample's recorded chain and writes every shadow query
+// of every level ([level][light pair][slot]: 32-B trace_stream records, thr < 0 = no query) with its
+// NdotL / NdotH, and one 16-B record per level; trace_stream answers the shadow queries; wf_combine
+// walks the levels back, adding the unshadowed light terms in the reference's order, and writes the
+// sample.
+struct WfArgs {
+  float4* rays;   // 2 per query slot: (o, thr), (d, 0); thr < 0: no query in this slot
+  float2* nl;     // per query slot: (NdotL, NdotH)
+  uint8_t* occ;   // per query slot: 1 = occluded (trace_stream)
+  float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
+  uint32_t n_slots;
+  int pairs;      // light-pair slots per level: n_lights * light_spp
+};
+
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
 struct TraceArgs {
   const float4* rays;          // 2 per query: (o.xyz, range threshold), (d.xyz, 0); shadow d is unit
@@ -197,6 +213,7 @@ struct TraceArgs {
   uint8_t* occ_out;            // shadow: 1 if occluded
   unsigned long long* stats;   // ST_* counters (stats launches only)
   int refill_min;
+  int sparse;                  // shadow queries with thr < 0 are empty slots: skipped, occ_out not written
 };
 
 struct ReduceArgs {

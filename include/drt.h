@@ -210,14 +210,20 @@ typedef struct {
   int32_t mode;
   int32_t persistent;
   int32_t tiles_in_shard;
-  int32_t passes;      /* 2: a frame of a scene without refraction as a pass over the closest-hit
-                          chains (in-order frames: a pixel's samples in order; AA frames of BVH / Grid
-                          scenes of >= 1024 objects whose whole frame has >= 2^23 samples or whose
-                          scene has >= 2^19 objects) and a pass over every sample with its closest
-                          hits read back; 1 otherwise.  The plan depends on the params and the
-                          uploaded scene only, and drt_render follows it.  Both plans render the
-                          same frame; the stats differ only in where shadow work is counted
-                          (shadow_* on the reference tree, wide_* on the shadow tree). */
+  int32_t passes;      /* 2: a pass over the samples' closest hits and a pass over every sample with
+                          its closest hits read back; 1 otherwise.  Two passes for: in-order frames
+                          (DoF / glossy) of scenes without refraction (a pixel's samples in order);
+                          AA frames of BVH / Grid scenes of >= 1024 objects whose whole frame has
+                          >= 2^23 samples or whose scene has >= 2^19 objects; Whitted frames of such
+                          scenes (quad light 0: at any size, one closest-hit chain per pixel shared
+                          by its gridRes light samples; point light: the AA size rule).  With a
+                          refracting material the AA / Whitted passes record each sample's whole
+                          closest-hit tree (<= 2^(max_depth+1) - 1 hits) if it fits 32 GB.  The
+                          plan depends on the params and the uploaded scene only, and drt_render
+                          follows it.  Both plans render the same frame; the stats differ only in
+                          where shadow work is counted (shadow_* on the reference tree, wide_* on
+                          the shadow tree) and, for quad-light Whitted frames, in closest_* (gridRes
+                          times fewer traversals). */
   int32_t reserved[4];
 } drt_frame_plan;
 int drt_plan_frame(const drt_ctx* ctx, const drt_frame_params* params, drt_frame_plan* out);
@@ -275,7 +281,8 @@ int drt_frame_spans(drt_ctx* ctx, int max_frames, double* path_start, double* pa
 /* The same frames' passes: a two-pass frame (drt_frame_plan.passes == 2) is the closest-chain pass
  * then the replay pass, timed from the path-kernel start to the end of the first launch and from
  * there to the path-kernel end (HIP events on the frame's stream; pass1 + pass2 = path_ms of
- * drt_frame_times).  A one-pass frame reports its path kernel as pass 1 and 0 for pass 2.  For a
+ * drt_frame_times).  A one-pass frame reports its path kernel as pass 1 and ~0 for pass 2 (two
+ * events recorded back to back: a few microseconds).  For a
  * frame rendered alone these are the launches' device times; with frames in flight a pass's span
  * also holds its waits for CU room.  Waits for those frames.  Returns the count written (>= 0). */
 int drt_frame_pass_times(drt_ctx* ctx, int max_frames, double* pass1_ms, double* pass2_ms);

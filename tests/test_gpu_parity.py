@@ -936,6 +936,53 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
     assert renderer.plan(renderer.frame_params(seed=4, **kw))["passes"] == (2 if first == "quad" else 1)
 
 
+
+@pytest.mark.parametrize("spp,first,light_spp,md", [(16, "quad", 1, 4), (16, "point", 4, 6), (9, "quad", 1, 1),
+                                                    (0, "quad", 1, 5), (0, "point", 1, 3)])
+def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, spp, first, light_spp, md):
+    """Pass 2 of an AA / Whitted two-pass BVH frame as a wavefront (round 5; drt_kernels.hpp WfArgs):
+    wf_gen writes every shadow query of every recorded level, trace_stream answers them on the shadow
+    tree, wf_combine adds the unshadowed light terms in the light loop's order and unwinds the mirror
+    chain.  The frame equals the persistent MODE_AREPLAY pass's (DRT_WAVEFRONT=0) and the
+    reference-order frame bit for bit, with the same shadow rays and shadow-tree work — AA with a quad
+    light first or last and 4 area samples per light, the depth cut at max_depth 1..6, Whitted frames."""
+    import bench
+
+    s = drt.Scene()
+    c = bench.CAMERA
+    s.set_camera(c["eye"], c["at"], c["up"], c["fovy"], c["hither"], 40, 36, 0.0, 1.0)
+    s.set_background((0.078, 0.361, 0.753))
+    s.set_accel("bvh")
+    s.set_spp(spp)
+    quad = ((4, 3, 2), (1, 1, 1), (4, 2, 2), (3, 3, 2), 16)
+    if first == "quad":
+        s.add_light_quad(*quad)
+        s.add_light_point((-3, 1, 5), (1, 1, 1))
+    else:
+        s.add_light_point((-3, 1, 5), (1, 1, 1))
+        s.add_light_quad(*quad)
+    s.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), 0.5, 30.0827, 0, 1)
+    s.add_triangles(bench.synthetic_triangles(20_000))
+    s.build()
+    renderer.upload(s)
+    kw = {"max_depth": md, "light_spp": light_spp}
+    assert renderer.plan(renderer.frame_params(seed=6, **kw))["passes"] == 2
+    wf = renderer.render(seed=6, stats=True, **kw)
+    st = renderer.stats()
+    monkeypatch.setenv("DRT_WAVEFRONT", "0")
+    pers = renderer.render(seed=6, stats=True, **kw)
+    st1 = renderer.stats()
+    ref = renderer.render(seed=6, stats=True, reference_order=True, **kw)
+    rst = renderer.stats()
+    np.testing.assert_array_equal(bits(wf), bits(pers))
+    np.testing.assert_array_equal(bits(wf), bits(ref))
+    assert st["samples"] == st1["samples"] == rst["samples"]
+    assert st["shadow_rays"] == st1["shadow_rays"] == rst["shadow_rays"] > 0
+    for k in ("closest_rays", "closest_inner", "closest_leaf", "closest_prims", "shadow_inner", "shadow_leaf",
+              "shadow_prims"):
+        assert st[k] == st1[k], k
+
+
 @pytest.mark.parametrize("accel,spp", [("bvh", 4), ("grid", 4), ("bvh", 0), ("grid", 0)])
 def test_refraction_two_pass_frame_equals_one_pass(drt, oracle_mod, renderer, tmp_path, monkeypatch, accel, spp):
     """AA and Whitted frames of scenes WITH a refracting material (glass spheres, trans 1) run in two
@@ -975,7 +1022,7 @@ def test_refraction_two_pass_frame_equals_one_pass(drt, oracle_mod, renderer, tm
 def test_frame_pass_times_split_the_path_time(drt, monkeypatch):
     """drt_frame_pass_times (round 5; bench.py roofline.passes): a two-pass frame's closest-chain and
     replay launches, timed on the frame's stream, add up to its path-kernel time; a one-pass frame
-    reports its kernel as pass 1 and 0 for pass 2."""
+    reports its kernel as pass 1 and ~0 for pass 2."""
     import bench
 
     s = drt.Scene()
@@ -993,7 +1040,8 @@ def test_frame_pass_times_split_the_path_time(drt, monkeypatch):
         path_ms, _ = r.frame_times(6)
         p1, p2 = r.frame_pass_times(6)
         assert len(p1) == len(p2) == 6
-        assert (p1 > 0).all() and (p2[:3] > 0).all() and (p2[3:] == 0).all()
+        # (a one-pass frame's pass-2 span is two events recorded back to back: a few microseconds)
+        assert (p1 > 0).all() and (p2[:3] > 0.05).all() and (p2[3:] < 0.05).all()
         np.testing.assert_allclose(p1 + p2, path_ms, rtol=1e-3, atol=2e-3)
     finally:
         r.close()
