@@ -269,7 +269,9 @@ def main():
     shard_p = shard_ps[0]
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
     ref_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, reference_order=True, **fkw)
-    passes = r.plan(shard_p)["passes"]
+    plan = r.plan(shard_p)
+    passes = plan["passes"]
+    wavefront = bool(plan.get("wavefront"))
     frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
     # frames in flight: frame i runs on stream / scratch slot / output buffers i % pipe, so the next
     # frame's kernel fills the CUs the previous frame's tail leaves idle
@@ -447,6 +449,9 @@ def main():
         for name, ms, b, pp in (("closest_chain", float(np.mean(pass1_ms)), b1, pmc_passes[0]),
                                 ("replay", float(np.mean(pass2_ms)), b2, pmc_passes[1])):
             row = {"pass": name, "ms": round(ms, 3), "bytes": int(b), "achieved": round(b / (ms * 1e-3) / 1e9, 1)}
+            if name == "replay":
+                row["kernels"] = ("wf_gen + trace_stream<shadow> + wf_combine" if wavefront else
+                                  f"path_persistent<{args.accel.upper()}> replay")
             if ceiling:
                 row["frac"] = round(row["achieved"] / ceiling["peak_GB_per_s"], 4)
             if pp and pp.get("read_bytes") is not None:
@@ -503,7 +508,10 @@ def main():
                      "valu_busy": round(valu_busy, 4) if valu_busy else None,
                      "pmc": pmc or None,
                      "two_level_model": model,
-                     "kernel": f"path_persistent<{args.accel.upper()}>", "bytes_per_launch": int(bytes_launch),
+                     "kernel": f"path_persistent<{args.accel.upper()}>" + (
+                         " closest chain + wavefront replay (wf_gen, trace_stream, wf_combine)" if wavefront else
+                         " closest chain + replay" if passes == 2 else ""),
+                     "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),
                      # §8(d)'s bytes (64 B per inner visit + 48 B per primitive test) on the reference's
                      # binary tree for every query (a DRT_FRAME_REFERENCE_ORDER stats frame): the basis

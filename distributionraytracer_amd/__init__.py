@@ -305,7 +305,7 @@ class Renderer:
         out = _lib.DrtFramePlan()
         check(_lib.load().drt_plan_frame(self.h, C.byref(params), C.byref(out)), self.h, "drt_plan_frame")
         return dict(work_items=int(out.work_items), sample_slots=int(out.sample_slots), mode=int(out.mode),
-                    persistent=bool(out.persistent), tiles_in_shard=int(out.tiles_in_shard), passes=int(out.passes))
+                    persistent=bool(out.persistent), tiles_in_shard=int(out.tiles_in_shard), passes=int(out.passes), wavefront=bool(out.wavefront))
 
     def render_device(self, params, d_out_ptr, stream=None):
         """Asynchronous: shard (or whole frame) into a device pointer on `stream` (int handle)."""

@@ -64,7 +64,7 @@ class DrtFrameStats(C.Structure):
 class DrtFramePlan(C.Structure):
     _fields_ = [("work_items", C.c_uint64), ("sample_slots", C.c_uint64), ("mode", C.c_int32),
                 ("persistent", C.c_int32), ("tiles_in_shard", C.c_int32), ("passes", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("wavefront", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class DrtLight(C.Structure):

@@ -914,6 +914,7 @@ struct Plan {
   uint32_t chain_div;   // two-pass Whitted frame: replay sample slots per closest-chain record (grid_res)
   bool tree;            // ... of a scene with a refracting material: MODE_TCHAIN + MODE_TREPLAY
   uint32_t recs;        // closest-hit records per (shared) sample: max_depth + 1, or 2^(max_depth+1) - 1
+  bool wavefront;       // AA / Whitted BVH two-pass frame without refraction: pass 2 as wf_gen + trace_stream + wf_combine
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -1071,6 +1072,17 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
         P.chain_div = 1;
       }
     }
+  }
+  // Pass 2 of an AA / Whitted BVH frame without refraction as a wavefront (round 5, WfArgs): every
+  // shadow query of the frame generated from the recorded chains, answered by the streaming kernel,
+  // combined per sample — 78.7 -> 69.3 ms on the headline (profiles/r05_ab_wavefront_replay.jsonl).
+  // DRT_WAVEFRONT=0 keeps the persistent MODE_AREPLAY pass, and so does a frame of >= 2^32 query slots
+  // or whose query buffers cannot be allocated (run_frame).  Both render the same frame.
+  P.wavefront = false;
+  if (P.aa_chain && !P.tree && c->accel == DRT_ACCEL_BVH && c->has_wide && env_int("DRT_WAVEFRONT", 1) != 0) {
+    const uint64_t q = ((uint64_t)md + 1u) * (uint64_t)c->lights.size() * (uint64_t)(F.light_spp > 0 ? F.light_spp : 1) *
+                       P.n_slots;
+    P.wavefront = P.n_slots < 0xFFFFFFFFull && q < 0xFFFFFF00ull;
   }
   ReduceArgs& R = P.R;
   R.nsub = slots;
@@ -1254,17 +1266,13 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());
     DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
-    // Pass 2 of an AA / Whitted BVH frame without refraction as a wavefront (round 5, WfArgs): every
-    // shadow query of the frame generated from the recorded chains, answered by the streaming kernel,
-    // combined per sample.  DRT_WAVEFRONT=0 keeps the persistent MODE_AREPLAY pass; a frame whose query
-    // array does not fit (2^32 query slots, device memory) keeps it too.  Both render the same frame.
+    // pass 2 as a wavefront (plan_frame): the query buffers, or the persistent replay if they do not fit
     bool wavefront = false;
     WfArgs W{};
-    if (P.aa_chain && !P.tree && c->accel == DRT_ACCEL_BVH && c->has_wide && env_int("DRT_WAVEFRONT", 1) != 0) {
+    if (P.wavefront) {
       const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = (uint64_t)c->lights.size() * (uint64_t)P.F.light_spp;
       const uint64_t q = levels * pairs * P.n_slots;
-      if (P.n_slots < 0xFFFFFFFFull && q < 0xFFFFFF00ull &&
-          c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+      if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.n_slots) == hipSuccess) {
@@ -1303,9 +1311,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         A.counter = F2.work_counter;
         A.occ_out = W.occ;
         A.stats = F2.stats;
-        A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 24);
+        // 7 waves / SIMD and refill at 16 idle lanes: 2 407 Mrays/s on the headline against 2 235 at the
+        // batched queries' 6 / 24 (8 / 16: 2 393-2 404, 7 / 8: 2 391-2 395; r05_wavefront_knobs_*.jsonl)
+        A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 16);
         A.sparse = 1;
-        launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 6), st);
+        launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);
         DRT_HIP(c, hipGetLastError());
       }
       launch_wf_combine(S, F2, W, st);
@@ -1360,6 +1370,7 @@ int drt_plan_frame(const drt_ctx* c, const drt_frame_params* p, drt_frame_plan* 
   out->persistent = P.persistent ? 1 : 0;
   out->tiles_in_shard = P.F.n_my_tiles;
   out->passes = P.two_pass ? 2 : 1;
+  out->wavefront = P.wavefront ? 1 : 0;
   return DRT_OK;
 }
 

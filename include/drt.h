@@ -224,7 +224,13 @@ typedef struct {
                           where shadow work is counted (shadow_* on the reference tree, wide_* on
                           the shadow tree) and, for quad-light Whitted frames, in closest_* (gridRes
                           times fewer traversals). */
-  int32_t reserved[4];
+  int32_t wavefront;   /* 1: pass 2 of this two-pass frame runs as a wavefront — every shadow query of
+                          the frame generated from the recorded closest hits, answered by the
+                          streaming traversal kernel, combined per sample (AA / Whitted frames of
+                          BVH scenes without refraction, < 2^32 query slots; DRT_WAVEFRONT=0: the
+                          persistent replay).  A frame whose query buffers cannot be allocated runs
+                          the persistent replay, which renders the same frame. */
+  int32_t reserved[3];
 } drt_frame_plan;
 int drt_plan_frame(const drt_ctx* ctx, const drt_frame_params* params, drt_frame_plan* out);
 

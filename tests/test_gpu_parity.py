@@ -966,10 +966,12 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, s
     s.build()
     renderer.upload(s)
     kw = {"max_depth": md, "light_spp": light_spp}
-    assert renderer.plan(renderer.frame_params(seed=6, **kw))["passes"] == 2
+    plan = renderer.plan(renderer.frame_params(seed=6, **kw))
+    assert plan["passes"] == 2 and plan["wavefront"]
     wf = renderer.render(seed=6, stats=True, **kw)
     st = renderer.stats()
     monkeypatch.setenv("DRT_WAVEFRONT", "0")
+    assert not renderer.plan(renderer.frame_params(seed=6, **kw))["wavefront"]
     pers = renderer.render(seed=6, stats=True, **kw)
     st1 = renderer.stats()
     ref = renderer.render(seed=6, stats=True, reference_order=True, **kw)

@@ -24,25 +24,40 @@ CALIB = ROOT / "profiles" / "r03_fetch_calibration.json"
 
 
 def dispatch_counters(pass_dir: Path):
-    """{(dispatch_id, kernel): {counter: value}} summed over the dispatch's rows."""
+    """{(dispatch_id, kernel): {counter: value}} summed over the dispatch's rows; the dispatch's queue
+    is kept under the key "__queue"."""
     out = {}
     for f in pass_dir.rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             key = (int(r["Dispatch_Id"]), r["Kernel_Name"])
-            d = out.setdefault(key, {})
+            d = out.setdefault(key, {"__queue": r.get("Queue_Id", "0")})
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return out
 
 
-def timed_path_dispatch(counters, sub=None):
-    # the timed frame is the LAST path_persistent dispatch of the non-stats instantiation
-    # (rocprofv3 reports demangled names: path_persistent<TRI_ONLY, STATS=false, MODE, WAVES, ACC>)
+def last_frame(counters, sub=None):
+    """Dispatch keys of the last timed frame: its non-stats path_persistent dispatch (pass 1, or the
+    whole one-pass frame), then on the same queue its second pass — the persistent replay (FrameMode
+    6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the non-stats trace_stream, wf_combine_kernel).
+    With `sub`, the last dispatch whose name holds it."""
     if sub:
         keys = sorted(k for k in counters if sub in k[1])
-    else:
-        keys = sorted(k for k in counters
-                      if "path_persistent<" in k[1] and k[1].split("<", 2)[1].split(",")[1].strip() == "false")
-    return keys[-1] if keys else None
+        return [keys[-1]] if keys else []
+    frames, cur = [], {}
+    for k in sorted(counters):
+        q, name, a = counters[k]["__queue"], k[1], _targs(k[1])
+        if "path_persistent<" in name:
+            if _stats(name):
+                cur[q] = None
+            elif _mode(name) in (6, 8, 10) and cur.get(q) is not None:
+                cur[q].append(k)
+            else:
+                cur[q] = [k]
+                frames.append(cur[q])
+        elif ("wf_gen_kernel" in name or "wf_combine_kernel" in name or
+              ("trace_stream<" in name and a and a[-1] == "false")) and cur.get(q) is not None:
+            cur[q].append(k)
+    return frames[-1] if frames else []
 
 
 def _targs(name):
@@ -60,6 +75,15 @@ def _mode(name):
 def _stats(name):
     a = _targs(name)
     return len(a) > 1 and a[1] == "true"
+
+
+def _sum(counters, keys):
+    out = {}
+    for k in keys:
+        for n, v in counters[k].items():
+            if n != "__queue":
+                out[n] = out.get(n, 0.0) + v
+    return out
 
 
 def derive(vals):
@@ -108,27 +132,20 @@ def main():
     out = Path(sys.argv[3]) if len(sys.argv) > 3 else ROOT / "profiles" / "pmc_traffic.json"
     sub = sys.argv[4] if len(sys.argv) > 4 else None
     vals, kernel = {}, None
-    pass_vals = [{}, {}]  # a two-pass frame's launches: the closest-chain pass, the replay pass
+    pass_vals = [{}, {}]  # a two-pass frame's launches: the closest-chain pass, the replay pass (all its launches)
     pass_kernels = [None, None]
     for p in sorted(x for x in root.iterdir() if x.is_dir()):
         c = dispatch_counters(p)
-        k = timed_path_dispatch(c, sub)
-        if k is None:
+        fr = last_frame(c, sub)
+        if not fr:
             continue
-        kernel = k[1]
-        cur = dict(c[k])
-        # a two-pass frame (FrameMode 5 or 7, then 6, drt_capi.hip): the frame is both launches
-        if _mode(k[1]) in (6, 8):
-            prev = [d for d in c if d[0] < k[0] and _mode(d[1]) in (5, 7) and not _stats(d[1])]
-            if prev:
-                p5 = max(prev)  # the frame's first pass
-                kernel = p5[1] + " + " + k[1]
-                pass_vals[0].update(c[p5])
-                pass_vals[1].update(c[k])
-                pass_kernels = [p5[1], k[1]]
-                for n, v in c[p5].items():
-                    cur[n] = cur.get(n, 0.0) + v
-        vals.update(cur)
+        kernel = " + ".join(k[1] for k in fr)
+        # this pass's counters summed over the frame's launches (each counter group is its own pass)
+        vals.update(_sum(c, fr))
+        if len(fr) > 1:
+            pass_kernels = [fr[0][1], " + ".join(k[1] for k in fr[1:])]
+            pass_vals[0].update(_sum(c, fr[:1]))
+            pass_vals[1].update(_sum(c, fr[1:]))
     rec = derive(vals)
     if "hbm_bytes_per_launch" not in rec:
         sys.exit(f"no read-byte counters under {root}: {sorted(vals)}")
