@@ -920,6 +920,13 @@ struct Plan {
 };
 
 static void note_last_path_ms(drt_ctx* c);
+// Shadow-query slots per level of a wavefront replay: the (light, k) pairs the light loop visits — every
+// k of a quad light, k = 0 of a point light (next_light_pair).
+static uint64_t wf_pairs(const drt_ctx* c, int light_spp) {
+  uint64_t n = 0;
+  for (const drt_light& l : c->lights) n += l.type == DRT_LIGHT_QUAD ? (uint64_t)std::max(1, light_spp) : 1u;
+  return n;
+}
 static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "no scene uploaded");
   const int shards = p->n_shards <= 0 ? 1 : p->n_shards;
@@ -1079,10 +1086,10 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // DRT_WAVEFRONT=0 keeps the persistent MODE_AREPLAY pass, and so does a frame of >= 2^32 query slots
   // or whose query buffers cannot be allocated (run_frame).  Both render the same frame.
   P.wavefront = false;
-  if (P.aa_chain && !P.tree && c->accel == DRT_ACCEL_BVH && c->has_wide && env_int("DRT_WAVEFRONT", 1) != 0) {
-    const uint64_t q = ((uint64_t)md + 1u) * (uint64_t)c->lights.size() * (uint64_t)(F.light_spp > 0 ? F.light_spp : 1) *
-                       P.n_slots;
-    P.wavefront = P.n_slots < 0xFFFFFFFFull && q < 0xFFFFFF00ull;
+  if (P.aa_chain && !P.tree && ((c->accel == DRT_ACCEL_BVH && c->has_wide) || c->accel == DRT_ACCEL_GRID) &&
+      env_int("DRT_WAVEFRONT", 1) != 0 && (c->accel == DRT_ACCEL_BVH || env_int("DRT_WAVEFRONT_GRID", 1) != 0)) {
+    const uint64_t q = ((uint64_t)md + 1u) * wf_pairs(c, F.light_spp) * P.n_slots;
+    P.wavefront = P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems;
   }
   ReduceArgs& R = P.R;
   R.nsub = slots;
@@ -1270,7 +1277,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     bool wavefront = false;
     WfArgs W{};
     if (P.wavefront) {
-      const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = (uint64_t)c->lights.size() * (uint64_t)P.F.light_spp;
+      const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
       const uint64_t q = levels * pairs * P.n_slots;
       if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
@@ -1283,6 +1290,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         W.lvl = c->d_wf_lvl_s[slot].as<float4>();
         W.n_slots = (uint32_t)P.n_slots;
         W.pairs = (int)pairs;
+        W.grid = c->accel == DRT_ACCEL_GRID ? 1 : 0;
       } else {
         (void)hipGetLastError();
         for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot]}) b->release();
@@ -1304,7 +1312,21 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       launch_wf_gen(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
       const uint64_t q = (uint64_t)(P.F.max_depth + 1) * (uint64_t)W.pairs * W.n_slots;
-      if (q) {
+      if (q && W.grid) {
+        // the Grid's shadow queries on its persistent stepper (MODE_QSTREAM): Grid::Traverse(Ray&)'s answer
+        // is tied to the cells its walk visits, so they stay on the Grid
+        FrameArgs FQ = F2;
+        FQ.mode = MODE_QSTREAM;
+        FQ.n_items = q;
+        FQ.part_items = (uint32_t)((q + 7) / 8);
+        FQ.q_rays = W.rays;
+        FQ.q_occ = W.occ;
+        FQ.process_min = 1;
+        FQ.refill_min = env_int("DRT_WAVEFRONT_GRID_REFILL_MIN", P.F.refill_min);
+        FQ.waves = env_int("DRT_WAVEFRONT_GRID_WAVES", 5);
+        launch_path_persistent(S, FQ, c->accel, c->tri_only, stats, st);
+        DRT_HIP(c, hipGetLastError());
+      } else if (q) {
         TraceArgs A{};
         A.rays = W.rays;
         A.n = (uint32_t)q;

@@ -2018,6 +2018,17 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     seq_start_sample<STATS, MODE, ACC>(S, F, L, C);
     return;
   }
+  if (MODE == MODE_QSTREAM) {  // work item = one shadow query of a wavefront replay
+    const float4 a = F.q_rays[2 * (size_t)item];
+    if (a.w < 0.0f) {  // an empty slot: no query
+      L.item = kNoItem;
+      return;
+    }
+    const float4 b = F.q_rays[2 * (size_t)item + 1];
+    L.fl = 0u;
+    start_query<STATS, ACC>(S, L, make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)), true, a.w, C);
+    return;
+  }
   if (MODE == MODE_PROG) {  // work item = pixel, one sample (main.cpp:540-572)
     const Item it = decode_item(F, S.res_x, S.res_y, item, 1);
     if (!it.valid) {
@@ -2274,7 +2285,10 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
       }
       if (done) {
         if (MODE == MODE_SEQ && part == kPartYield) L.fl |= LF_YIELD;
-        if constexpr (MODE == MODE_SKEL) skel_process<STATS, ACC>(S, F, L, C);
+        if constexpr (MODE == MODE_QSTREAM) {  // the query's answer (a Grid miss of the grid box: shadowed)
+          F.q_occ[L.item] = (L.fl & LF_HIT) ? 1 : 0;
+          L.item = kNoItem;
+        } else if constexpr (MODE == MODE_SKEL) skel_process<STATS, ACC>(S, F, L, C);
         else if constexpr (MODE == MODE_CHAIN) chain_process<STATS, ACC>(S, F, L, C);
         else lane_process<STATS, MODE, ACC>(S, F, L, fs, C);
       }
@@ -2475,12 +2489,9 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
       const uint32_t mat = prim_material(S.prims[3 * prim]);
       const V3 V = neg(normalize(q.d));
       V3 lightPos = mk(0, 0, 0);
-      for (int j = 0; j < np; j++) {  // setup_shadow for every pair the light loop visits
-        const size_t qi = ((size_t)l * np + j) * ns + slot;
-        if (!wf_pair_used(S, F, j)) {
-          W.rays[2 * qi] = make_float4(0.f, 0.f, 0.f, -1.0f);
-          continue;
-        }
+      for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // setup_shadow for every pair the light loop visits
+        if (!wf_pair_used(S, F, j)) continue;
+        const size_t qi = ((size_t)l * np + u++) * ns + slot;
         const int li = light_of_pair(j, F);
         lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
         V3 Lv = sub(lightPos, hitP);
@@ -2489,8 +2500,10 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
         const V3 H = normalize(add(Lv, V));
         const float NdotL = smax(dot(N, Lv), 0.0f), NdotH = smax(dot(N, H), 0.0f);
         const V3 so = add(hitP, mul(N, 1e-4f));
-        const V3 sd = normalize(Ls);
-        W.rays[2 * qi] = make_float4(so.x, so.y, so.z, shadow_threshold(length(Ls)));
+        // BVH::Traverse(Ray&) normalises Ls, range |Ls| + EPSILON; Grid::Traverse(Ray&) gets the unit L,
+        // range |L|, direction re-normalised (Q1; setup_shadow)
+        const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
+        W.rays[2 * qi] = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
         W.rays[2 * qi + 1] = make_float4(sd.x, sd.y, sd.z, 0.0f);
         W.nl[qi] = make_float2(NdotL, NdotH);
       }
@@ -2553,9 +2566,10 @@ __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs 
     }
     const drt_material m = S.mats[mat];
     V3 acc = mk(0, 0, 0);
-    for (int j = 0; j < np; j++) {  // main.cpp:444-450, in the light loop's order
-      const size_t qi = ((size_t)l * np + j) * ns + slot;
-      if (!wf_pair_used(S, F, j) || W.occ[qi]) continue;
+    for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // main.cpp:444-450, in the light loop's order
+      if (!wf_pair_used(S, F, j)) continue;
+      const size_t qi = ((size_t)l * np + u++) * ns + slot;
+      if (W.occ[qi]) continue;
       const float2 nl = W.nl[qi];
       acc = add(acc, light_term(m, nl.x, nl.y, S.lights[light_of_pair(j, F)], F));
     }
@@ -2780,6 +2794,7 @@ static void launch_persistent_t(const SceneArgs& S, const FrameArgs& F, hipStrea
     case MODE_AREPLAY: launch_persistent_m<T, ST, MODE_AREPLAY, A>(S, F, st); break;
     case MODE_TCHAIN: launch_persistent_m<T, ST, MODE_TCHAIN, A>(S, F, st); break;
     case MODE_TREPLAY: launch_persistent_m<T, ST, MODE_TREPLAY, A>(S, F, st); break;
+    case MODE_QSTREAM: if constexpr (A == ACC_GRID) launch_persistent_m<T, ST, MODE_QSTREAM, A>(S, F, st); break;
     case MODE_CHAIN: launch_persistent_m<T, ST, MODE_CHAIN, A>(S, F, st); break;
     case MODE_PROG: launch_persistent_m<T, ST, MODE_PROG, A>(S, F, st); break;
     default: launch_persistent_m<T, ST, MODE_WHITTED_POINT, A>(S, F, st); break;

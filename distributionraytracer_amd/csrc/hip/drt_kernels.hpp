@@ -34,8 +34,11 @@ enum FrameMode : int {
   // closest hits form a binary tree (refraction child first, then reflection, main.cpp:465-512):
   MODE_TCHAIN = 9,   // pass 1: the whole tree of closest-hit queries, no shadow rays, each hit recorded
                      // in the order rayTracing() makes the queries (<= 2^(max_depth+1) - 1 per sample)
-  MODE_TREPLAY = 10  // pass 2: the whole rayTracing() with refraction, the closest hits read back in
-                     // that order, shadow queries on the shadow tree / the Grid
+  MODE_TREPLAY = 10,  // pass 2: the whole rayTracing() with refraction, the closest hits read back in
+                      // that order, shadow queries on the shadow tree / the Grid
+  // The Grid's wavefront replay (round 5, WfArgs): one Grid::Traverse(Ray&) shadow query per work item
+  // from FrameArgs::q_rays (thr < 0: no query), its answer to q_occ
+  MODE_QSTREAM = 11
 };
 
 enum StatSlot : int {
@@ -180,6 +183,9 @@ struct FrameArgs {
   // MODE_TCHAIN / MODE_TREPLAY: records per sample (2^(max_depth+1) - 1); a lane's rk holds its next
   // record index
   int tree_recs;
+  // MODE_QSTREAM: 2 float4 per query ((o, range), (d, 0)), 1 byte per answer (1 = shadowed)
+  const float4* q_rays;
+  uint8_t* q_occ;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per
@@ -190,7 +196,7 @@ constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 192;
 // Wavefront replay of an AA / Whitted two-pass BVH frame without refraction (round 5): the closest hits
 // are all known after MODE_CHAIN, so every shading decision except occlusion is a function of them.
 // wf_gen (one thread per sample slot) walks each sample's recorded chain and writes every shadow query
-// of every level ([level][light pair][slot]: 32-B trace_stream records, thr < 0 = no query) with its
+// of every level ([level][visited light pair][slot]: 32-B trace_stream records, thr < 0 = no query) with its
 // NdotL / NdotH, and one 16-B record per level; trace_stream answers the shadow queries; wf_combine
 // walks the levels back, adding the unshadowed light terms in the reference's order, and writes the
 // sample.
@@ -200,7 +206,8 @@ struct WfArgs {
   uint8_t* occ;   // per query slot: 1 = occluded (trace_stream)
   float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
   uint32_t n_slots;
-  int pairs;      // light-pair slots per level: n_lights * light_spp
+  int grid;       // Grid scene: queries as Grid::Traverse(Ray&) takes them (unit L, range |L|)
+  int pairs;      // query slots per level: the (light, k) pairs the light loop visits (a point light: k = 0 only)
 };
 
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.

@@ -937,22 +937,24 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
 
 
 
-@pytest.mark.parametrize("spp,first,light_spp,md", [(16, "quad", 1, 4), (16, "point", 4, 6), (9, "quad", 1, 1),
-                                                    (0, "quad", 1, 5), (0, "point", 1, 3)])
-def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, spp, first, light_spp, md):
+@pytest.mark.parametrize("accel,spp,first,light_spp,md", [
+    ("bvh", 16, "quad", 1, 4), ("bvh", 16, "point", 4, 6), ("bvh", 9, "quad", 1, 1), ("bvh", 0, "quad", 1, 5),
+    ("bvh", 0, "point", 1, 3), ("grid", 16, "quad", 1, 4), ("grid", 9, "point", 4, 2), ("grid", 0, "quad", 1, 3)])
+def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, accel, spp, first, light_spp, md):
     """Pass 2 of an AA / Whitted two-pass BVH frame as a wavefront (round 5; drt_kernels.hpp WfArgs):
     wf_gen writes every shadow query of every recorded level, trace_stream answers them on the shadow
     tree, wf_combine adds the unshadowed light terms in the light loop's order and unwinds the mirror
     chain.  The frame equals the persistent MODE_AREPLAY pass's (DRT_WAVEFRONT=0) and the
     reference-order frame bit for bit, with the same shadow rays and shadow-tree work — AA with a quad
-    light first or last and 4 area samples per light, the depth cut at max_depth 1..6, Whitted frames."""
+    light first or last and 4 area samples per light, the depth cut at max_depth 1..6, Whitted frames.
+    On the Grid the queries run on its persistent stepper (MODE_QSTREAM), with the same cell work."""
     import bench
 
     s = drt.Scene()
     c = bench.CAMERA
     s.set_camera(c["eye"], c["at"], c["up"], c["fovy"], c["hither"], 40, 36, 0.0, 1.0)
     s.set_background((0.078, 0.361, 0.753))
-    s.set_accel("bvh")
+    s.set_accel(accel)
     s.set_spp(spp)
     quad = ((4, 3, 2), (1, 1, 1), (4, 2, 2), (3, 3, 2), 16)
     if first == "quad":
