@@ -914,7 +914,9 @@ struct Plan {
   uint32_t chain_div;   // two-pass Whitted frame: replay sample slots per closest-chain record (grid_res)
   bool tree;            // ... of a scene with a refracting material: MODE_TCHAIN + MODE_TREPLAY
   uint32_t recs;        // closest-hit records per (shared) sample: max_depth + 1, or 2^(max_depth+1) - 1
-  bool wavefront;       // AA / Whitted BVH two-pass frame without refraction: pass 2 as wf_gen + trace_stream + wf_combine
+  bool wavefront;       // two-pass frame without refraction: pass 2 as wf_gen + shadow-query stream + wf_combine
+  uint64_t wf_chunk;    // ... over chunks of this many sample slots
+  uint32_t wf_chunks;
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -1085,11 +1087,25 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // combined per sample — 78.7 -> 69.3 ms on the headline (profiles/r05_ab_wavefront_replay.jsonl).
   // DRT_WAVEFRONT=0 keeps the persistent MODE_AREPLAY pass, and so does a frame of >= 2^32 query slots
   // or whose query buffers cannot be allocated (run_frame).  Both render the same frame.
+  // In-order (DoF / glossy) two-pass frames too: wf_gen draws each sample's lens and reflectDir samples
+  // from its recorded stream position as MODE_REPLAY does.  The frame's sample slots go through pass 2 in
+  // chunks of DRT_WAVEFRONT_CHUNK_SLOTS (default 2^24: the headline in one, C4's 67 M slots in four), so
+  // the query buffers stay at (max_depth + 1) x pairs x 41 B + (max_depth + 1) x 16 B per chunk slot
+  // (C4: 14.8 GB per frame slot).
   P.wavefront = false;
-  if (P.aa_chain && !P.tree && ((c->accel == DRT_ACCEL_BVH && c->has_wide) || c->accel == DRT_ACCEL_GRID) &&
-      env_int("DRT_WAVEFRONT", 1) != 0 && (c->accel == DRT_ACCEL_BVH || env_int("DRT_WAVEFRONT_GRID", 1) != 0)) {
-    const uint64_t q = ((uint64_t)md + 1u) * wf_pairs(c, F.light_spp) * P.n_slots;
-    P.wavefront = P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems;
+  P.wf_chunk = 0;
+  P.wf_chunks = 0;
+  if (P.two_pass && !P.tree && (c->accel == DRT_ACCEL_BVH || c->accel == DRT_ACCEL_GRID) &&
+      env_int("DRT_WAVEFRONT", 1) != 0 && (c->accel == DRT_ACCEL_BVH || env_int("DRT_WAVEFRONT_GRID", 1) != 0) &&
+      (P.aa_chain || env_int("DRT_WAVEFRONT_INORDER", 1) != 0)) {
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(P.n_slots, env_u64("DRT_WAVEFRONT_CHUNK_SLOTS", 1ull << 24)));
+    const uint64_t q = ((uint64_t)md + 1u) * wf_pairs(c, F.light_spp) * chunk;
+    const uint64_t chunks = (P.n_slots + chunk - 1) / chunk;
+    if (P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems && chunks <= 64) {
+      P.wavefront = true;
+      P.wf_chunk = chunk;
+      P.wf_chunks = (uint32_t)chunks;
+    }
   }
   ReduceArgs& R = P.R;
   R.nsub = slots;
@@ -1211,8 +1227,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     // 8 partition counters, 64 B apart, per pass: a two-pass frame's second pass uses the second
     // KiB, zeroed here too, so that no fill kernel sits between the passes (a fill waits for a CU
     // slot behind the other frames' persistent blocks, and the second pass behind it)
-    DRT_HIP(c, d_counter.ensure(2048));
-    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, P.two_pass ? 2048 : 1024, st));
+    // (a wavefront pass 2: one KiB of counters per chunk, from the second KiB on)
+    const size_t counter_bytes = 1024u * (1u + (P.two_pass ? std::max<uint32_t>(1u, P.wf_chunks) : 0u));
+    DRT_HIP(c, d_counter.ensure(std::max<size_t>(2048, counter_bytes)));
+    DRT_HIP(c, hipMemsetAsync(d_counter.p, 0, counter_bytes, st));
     P.F.work_counter = d_counter.as<unsigned int>();
     P.F.part_items = (uint32_t)((P.F.n_items + 7) / 8);
     P.F.refill_min = env_int("DRT_REFILL_MIN", 8);
@@ -1278,19 +1296,19 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     WfArgs W{};
     if (P.wavefront) {
       const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
-      const uint64_t q = levels * pairs * P.n_slots;
+      const uint64_t q = levels * pairs * P.wf_chunk;
       if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.n_slots) == hipSuccess) {
+          c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
         wavefront = true;
         W.rays = c->d_wf_rays_s[slot].as<float4>();
         W.nl = c->d_wf_nl_s[slot].as<float2>();
         W.occ = c->d_wf_occ_s[slot].as<uint8_t>();
         W.lvl = c->d_wf_lvl_s[slot].as<float4>();
-        W.n_slots = (uint32_t)P.n_slots;
         W.pairs = (int)pairs;
         W.grid = c->accel == DRT_ACCEL_GRID ? 1 : 0;
+        W.inorder = P.aa_chain ? 0 : 1;
       } else {
         (void)hipGetLastError();
         for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot]}) b->release();
@@ -1308,10 +1326,13 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     F2.work_counter = d_counter.as<unsigned int>() + 256;
-    if (wavefront) {
+    for (uint32_t k = 0; wavefront && k < P.wf_chunks; k++) {
+      W.slot0 = (uint32_t)(k * P.wf_chunk);
+      W.n_slots = (uint32_t)std::min<uint64_t>(P.wf_chunk, P.n_slots - W.slot0);
       launch_wf_gen(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
       const uint64_t q = (uint64_t)(P.F.max_depth + 1) * (uint64_t)W.pairs * W.n_slots;
+      unsigned int* counter = d_counter.as<unsigned int>() + 256u * (1u + k);
       if (q && W.grid) {
         // the Grid's shadow queries on its persistent stepper (MODE_QSTREAM): Grid::Traverse(Ray&)'s answer
         // is tied to the cells its walk visits, so they stay on the Grid
@@ -1321,6 +1342,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         FQ.part_items = (uint32_t)((q + 7) / 8);
         FQ.q_rays = W.rays;
         FQ.q_occ = W.occ;
+        FQ.work_counter = counter;
         FQ.process_min = 1;
         FQ.refill_min = env_int("DRT_WAVEFRONT_GRID_REFILL_MIN", P.F.refill_min);
         FQ.waves = env_int("DRT_WAVEFRONT_GRID_WAVES", 5);
@@ -1330,7 +1352,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         TraceArgs A{};
         A.rays = W.rays;
         A.n = (uint32_t)q;
-        A.counter = F2.work_counter;
+        A.counter = counter;
         A.occ_out = W.occ;
         A.stats = F2.stats;
         // 7 waves / SIMD and refill at 16 idle lanes: 2 407 Mrays/s on the headline against 2 235 at the
@@ -1341,9 +1363,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         DRT_HIP(c, hipGetLastError());
       }
       launch_wf_combine(S, F2, W, st);
-    } else {
-      launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
+      DRT_HIP(c, hipGetLastError());
     }
+    if (!wavefront) launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
   } else if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
     else launch_path(S, P.F, c->accel, c->tri_only, stats, st);

@@ -2446,24 +2446,35 @@ __device__ __forceinline__ bool wf_pair_used(const SceneArgs& S, const FrameArgs
 }
 
 __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
-  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // the slot's place in this chunk's buffers
   if (slot >= W.n_slots) return;
+  const uint32_t g = W.slot0 + slot;  // the frame's sample slot
   const size_t ns = W.n_slots;
   const int md = F.max_depth, np = W.pairs;
-  const Item it = decode_item(F, S.res_x, S.res_y, slot, F.nsub);
+  const Item it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
   int l = 0;
   if (it.valid) {
-    const uint32_t rec = F.chain_div > 1 ? (slot - (uint32_t)it.sub) / (uint32_t)F.chain_div : slot;
-    // the sample's primary ray and light sample (seq_start_sample, MODE_AREPLAY)
+    const uint32_t rec = F.chain_div > 1 ? (g - (uint32_t)it.sub) / (uint32_t)F.chain_div : g;
+    const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+    // an in-order frame's keyed stream from the sample's recorded position (MODE_REPLAY); an AA / Whitted
+    // frame draws nothing after the prologue (Q16)
+    uint32_t rk = W.inorder ? F.skel_rk[g] : 0u;
+    // the sample's primary ray and light sample (seq_start_sample, MODE_AREPLAY / MODE_REPLAY)
     RayP q;
     V3 ls;
     if (F.spp > 0) {
-      const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
-      const uint32_t pixel = slot / (uint32_t)F.nsub;
+      const uint32_t pixel = g / (uint32_t)F.nsub;
       float rx, ry, sx, sy;
       const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + it.sub] : shuffle_source(F, pmix, it.sub);
       sample_prologue_at(F, pmix, it.sub, pos, rx, ry, sx, sy);
-      q = primary_ray(S, (float)it.x + rx, (float)it.y + ry);
+      const float px = (float)it.x + rx, py = (float)it.y + ry;
+      if (W.inorder && F.dof) {
+        KRng rng{F.seed, pmix, rk};
+        q = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
+        rk = rng.k;
+      } else {
+        q = primary_ray(S, px, py);
+      }
       ls = mk(sx, sy, 0.0f);
     } else {
       const int sb = it.sub;
@@ -2520,8 +2531,15 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
         const V3 Vt = sub(mul(N, dot(V, N)), V);
         const float sin_t = eta * length(Vt);
         if (m.trans > 0.0f && sin_t >= 1.0f) kr = 1.0f;  // (trans == 1 never reaches a two-pass frame)
-        if (m.ks > 0.0f) {
-          const V3 R = normalize(sub(mul(mul(N, dot(V, N)), 2.0f), V));
+        if (m.ks > 0.0f) {  // reflectDir (reflect_dir)
+          V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
+          if (W.inorder) {
+            KRng rng{F.seed, pmix, rk};
+            R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
+            rk = rng.k;
+          } else {
+            R = normalize(R);
+          }
           flags = WF_REFL | (dot(R, N) > 0.0f ? WF_RN : 0u) | (kr == 1.0f && m.refl != 1.0f ? WF_KR1 : 0u);
           q = make_ray(add(hitP, mul(N, 1e-4f)), R);
           ls = lightPos;
@@ -2543,11 +2561,12 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
 __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= W.n_slots) return;
+  const uint32_t g = W.slot0 + slot;
   const size_t ns = W.n_slots;
   const int md = F.max_depth, np = W.pairs;
-  const Item it = decode_item(F, S.res_x, S.res_y, slot, F.nsub);
+  const Item it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
   if (!it.valid) {  // padding of a partial tile
-    F.samples[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+    F.samples[g] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
   // the last level of the chain: a miss, the depth cut, or a hit without a mirror child
@@ -2583,7 +2602,7 @@ __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs 
       c = cclamp(acc);
     }
   }
-  F.samples[slot] = make_float4(c.x, c.y, c.z, 0.0f);
+  F.samples[g] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
 void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {

@@ -205,7 +205,9 @@ struct WfArgs {
   float2* nl;     // per query slot: (NdotL, NdotH)
   uint8_t* occ;   // per query slot: 1 = occluded (trace_stream)
   float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
-  uint32_t n_slots;
+  uint32_t n_slots;  // sample slots of this chunk of the frame (the buffers' slot dimension)
+  uint32_t slot0;    // the chunk's first sample slot
+  int inorder;       // an in-order (DoF / glossy) frame: keyed-stream draws from FrameArgs::skel_rk (MODE_REPLAY)
   int grid;       // Grid scene: queries as Grid::Traverse(Ray&) takes them (unit L, range |L|)
   int pairs;      // query slots per level: the (light, k) pairs the light loop visits (a point light: k = 0 only)
 };

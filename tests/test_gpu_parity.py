@@ -937,17 +937,26 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
 
 
 
-@pytest.mark.parametrize("accel,spp,first,light_spp,md", [
-    ("bvh", 16, "quad", 1, 4), ("bvh", 16, "point", 4, 6), ("bvh", 9, "quad", 1, 1), ("bvh", 0, "quad", 1, 5),
-    ("bvh", 0, "point", 1, 3), ("grid", 16, "quad", 1, 4), ("grid", 9, "point", 4, 2), ("grid", 0, "quad", 1, 3)])
-def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, accel, spp, first, light_spp, md):
+@pytest.mark.parametrize("accel,spp,first,light_spp,md,rough,chunk", [
+    ("bvh", 16, "quad", 1, 4, 0, 0), ("bvh", 16, "point", 4, 6, 0, 0), ("bvh", 9, "quad", 1, 1, 0, 0),
+    ("bvh", 0, "quad", 1, 5, 0, 0), ("bvh", 0, "point", 1, 3, 0, 0), ("grid", 16, "quad", 1, 4, 0, 0),
+    ("grid", 9, "point", 4, 2, 0, 0), ("grid", 0, "quad", 1, 3, 0, 0),
+    # in-order frames (glossy: MODE_SKEL + MODE_REPLAY's keyed-stream draws), and pass 2 in chunks
+    ("bvh", 16, "quad", 1, 8, 0.1, 0), ("bvh", 0, "point", 1, 4, 0.2, 0), ("grid", 9, "quad", 1, 3, 0.2, 0),
+    ("bvh", 16, "quad", 4, 4, 0, 5000), ("bvh", 9, "point", 1, 6, 0.1, 7777), ("grid", 16, "quad", 1, 3, 0, 9000)])
+def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, accel, spp, first, light_spp, md, rough,
+                                                   chunk):
     """Pass 2 of an AA / Whitted two-pass BVH frame as a wavefront (round 5; drt_kernels.hpp WfArgs):
     wf_gen writes every shadow query of every recorded level, trace_stream answers them on the shadow
     tree, wf_combine adds the unshadowed light terms in the light loop's order and unwinds the mirror
     chain.  The frame equals the persistent MODE_AREPLAY pass's (DRT_WAVEFRONT=0) and the
     reference-order frame bit for bit, with the same shadow rays and shadow-tree work — AA with a quad
-    light first or last and 4 area samples per light, the depth cut at max_depth 1..6, Whitted frames.
+    light first or last and 4 area samples per light, the depth cut at max_depth 1..8, Whitted frames,
+    in-order (glossy) frames whose lens and reflectDir draws wf_gen takes from the recorded stream
+    positions, and pass 2 in chunks of sample slots (DRT_WAVEFRONT_CHUNK_SLOTS, a partial last chunk).
     On the Grid the queries run on its persistent stepper (MODE_QSTREAM), with the same cell work."""
+    if chunk:
+        monkeypatch.setenv("DRT_WAVEFRONT_CHUNK_SLOTS", str(chunk))
     import bench
 
     s = drt.Scene()
@@ -967,7 +976,7 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, a
     s.add_triangles(bench.synthetic_triangles(20_000))
     s.build()
     renderer.upload(s)
-    kw = {"max_depth": md, "light_spp": light_spp}
+    kw = {"max_depth": md, "light_spp": light_spp, "roughness": rough}
     plan = renderer.plan(renderer.frame_params(seed=6, **kw))
     assert plan["passes"] == 2 and plan["wavefront"]
     wf = renderer.render(seed=6, stats=True, **kw)
