@@ -38,7 +38,8 @@ def dispatch_counters(pass_dir: Path):
 def last_frame(counters, sub=None):
     """Dispatch keys of the last timed frame: its non-stats path_persistent dispatch (pass 1, or the
     whole one-pass frame), then on the same queue its second pass — the persistent replay (FrameMode
-    6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the non-stats trace_stream, wf_combine_kernel).
+    6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the non-stats trace_stream or the Grid's
+    MODE_QSTREAM (11) dispatch, wf_combine_kernel; per chunk of sample slots).
     With `sub`, the last dispatch whose name holds it."""
     if sub:
         keys = sorted(k for k in counters if sub in k[1])
@@ -49,7 +50,7 @@ def last_frame(counters, sub=None):
         if "path_persistent<" in name:
             if _stats(name):
                 cur[q] = None
-            elif _mode(name) in (6, 8, 10) and cur.get(q) is not None:
+            elif _mode(name) in (6, 8, 10, 11) and cur.get(q) is not None:
                 cur[q].append(k)
             else:
                 cur[q] = [k]

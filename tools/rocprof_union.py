@@ -33,8 +33,9 @@ def main():
         settle = json.loads(Path(a.bench_json).read_text())["config"].get("settle_frames", 0)
     settle = settle or 0
     # A frame is its non-stats path_persistent dispatch plus, on the same stream, the dispatches of its
-    # second pass: the persistent replay (FrameMode 6 / 8 / 10) or the wavefront replay (wf_gen_kernel,
-    # the non-stats trace_stream, wf_combine_kernel).  Frames in flight interleave across streams.
+    # second pass: the persistent replay (FrameMode 6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the
+    # non-stats trace_stream or the Grid's MODE_QSTREAM (11) dispatch, wf_combine_kernel; per chunk of
+    # sample slots).  Frames in flight interleave across streams.
     rows = []
     for f in Path(a.trace_dir).rglob("*kernel_trace.csv"):
         for r in csv.DictReader(open(f)):
@@ -49,7 +50,7 @@ def main():
             mode = int(targs[2]) if targs[2].strip().isdigit() else -1
             if stats:
                 cur[stream] = None
-            elif mode in (6, 8, 10) and cur.get(stream) is not None:
+            elif mode in (6, 8, 10, 11) and cur.get(stream) is not None:
                 cur[stream].append((s0, e0, k))
             else:
                 cur[stream] = [(s0, e0, k)]
