@@ -186,8 +186,11 @@ def main():
                     help="after timing, rank 0 checks the assembled frame against a whole-frame render (bitwise)")
     ap.add_argument("--frames-in-flight", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="frames pipelined on separate streams and scratch slots, so that a frame's start "
-                         "overlaps the previous frame's tail (0: 2 on one GPU, 3 on several, where a "
-                         "rank's shard is short and the tail a larger share of it)")
+                         "overlaps the previous frame's tail (0: 1 on one GPU, 2 on several.  Round 5, "
+                         "wavefront replay: a whole frame alone 62.4 ms, two in flight 65.3 ms per frame — "
+                         "the next frame's persistent chain pass holds the CUs the replay launches wait for; "
+                         "a rank's 1/8 shard 10.1 ms alone, 8.87 ms with two in flight, 8.83 with three, "
+                         "profiles/r05_frames_in_flight.jsonl, r05_shard_scaling_pipe*.json)")
     ap.add_argument("--settle-s", type=float, default=1.0,
                     help="untimed frames before the warmup steps until this much wall time has passed: the "
                          "GPU's clocks settle after the idle scene build (measured: with 2 warmup frames the "
@@ -264,7 +267,7 @@ def main():
     sptr = stream.cuda_stream
 
     fkw = {"max_depth": args.max_depth, "roughness": args.roughness, "light_spp": args.light_spp}
-    pipe = args.frames_in_flight or (3 if world >= 2 else 2)
+    pipe = args.frames_in_flight or (2 if world >= 2 else 1)
     shard_ps = [r.frame_params(seed=args.seed, shard=rank, n_shards=world, slot=j, **fkw) for j in range(pipe)]
     shard_p = shard_ps[0]
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
