@@ -186,7 +186,8 @@ def main():
                     help="after timing, rank 0 checks the assembled frame against a whole-frame render (bitwise)")
     ap.add_argument("--frames-in-flight", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="frames pipelined on separate streams and scratch slots, so that a frame's start "
-                         "overlaps the previous frame's tail (0: 1 on one GPU, 2 on several.  Round 5, "
+                         "overlaps the previous frame's tail (0: 1 for a wavefront AA / Whitted frame on one "
+                         "GPU, 2 otherwise.  Round 5, "
                          "wavefront replay: a whole frame alone 62.4 ms, two in flight 65.3 ms per frame — "
                          "the next frame's persistent chain pass holds the CUs the replay launches wait for; "
                          "a rank's 1/8 shard 10.1 ms alone, 8.87 ms with two in flight, 8.83 with three, "
@@ -267,14 +268,18 @@ def main():
     sptr = stream.cuda_stream
 
     fkw = {"max_depth": args.max_depth, "roughness": args.roughness, "light_spp": args.light_spp}
-    pipe = args.frames_in_flight or (2 if world >= 2 else 1)
+    plan = r.plan(r.frame_params(seed=args.seed, shard=rank, n_shards=world, **fkw))
+    passes = plan["passes"]
+    wavefront = bool(plan.get("wavefront"))
+    # frames in flight (--frames-in-flight 0): one on one GPU for a wavefront AA / Whitted frame, whose next
+    # frame's chain pass would hold the CUs its replay launches wait for; two otherwise — one-pass frames
+    # (C2, 1 ms: launch gaps) and in-order frames (C4: the chain pass's in-order tail) gain from the overlap,
+    # and so does a rank's shard on several GPUs (profiles/r05_frames_in_flight.jsonl, r05_configs_pipe*.jsonl)
+    pipe = args.frames_in_flight or (1 if world == 1 and wavefront and plan["mode"] != 1 else 2)
     shard_ps = [r.frame_params(seed=args.seed, shard=rank, n_shards=world, slot=j, **fkw) for j in range(pipe)]
     shard_p = shard_ps[0]
     stats_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, **fkw)
     ref_p = r.frame_params(seed=args.seed, shard=rank, n_shards=world, stats=True, reference_order=True, **fkw)
-    plan = r.plan(shard_p)
-    passes = plan["passes"]
-    wavefront = bool(plan.get("wavefront"))
     frame = torch.empty((args.res, args.res, 3), dtype=torch.float32, device="cuda")
     # frames in flight: frame i runs on stream / scratch slot / output buffers i % pipe, so the next
     # frame's kernel fills the CUs the previous frame's tail leaves idle
