@@ -1099,7 +1099,7 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
       env_int("DRT_WAVEFRONT", 1) != 0 && (c->accel == DRT_ACCEL_BVH || env_int("DRT_WAVEFRONT_GRID", 1) != 0) &&
       (P.aa_chain || env_int("DRT_WAVEFRONT_INORDER", 1) != 0)) {
     const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(P.n_slots, env_u64("DRT_WAVEFRONT_CHUNK_SLOTS", 1ull << 24)));
-    const uint64_t q = ((uint64_t)md + 1u) * wf_pairs(c, F.light_spp) * chunk;
+    const uint64_t q = ((uint64_t)md + 1u) * wf_pairs(c, F.light_spp) * (chunk + 8u);
     const uint64_t chunks = (P.n_slots + chunk - 1) / chunk;
     if (P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems && chunks <= 64) {
       P.wavefront = true;
@@ -1296,7 +1296,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     WfArgs W{};
     if (P.wavefront) {
       const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
-      const uint64_t q = levels * pairs * P.wf_chunk;
+      const uint64_t q = levels * pairs * (P.wf_chunk + 8u);  // (+ the last band's padding, wf_q)
       if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
@@ -1307,6 +1307,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         W.occ = c->d_wf_occ_s[slot].as<uint8_t>();
         W.lvl = c->d_wf_lvl_s[slot].as<float4>();
         W.pairs = (int)pairs;
+        W.levels = (int)levels;
         W.grid = c->accel == DRT_ACCEL_GRID ? 1 : 0;
         W.inorder = P.aa_chain ? 0 : 1;
       } else {
@@ -1329,9 +1330,15 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     for (uint32_t k = 0; wavefront && k < P.wf_chunks; k++) {
       W.slot0 = (uint32_t)(k * P.wf_chunk);
       W.n_slots = (uint32_t)std::min<uint64_t>(P.wf_chunk, P.n_slots - W.slot0);
+      // XCD bands (wf_q): DRT_WAVEFRONT_BANDS (1 or 8) consecutive ranges of the chunk's sample slots, each
+      // streamed first by one XCD.  BVH 8: headline +0.2 %, C3 +0.8 %; the Grid's MODE_QSTREAM measured
+      // 6 % slower with them and keeps 1 (profiles/r05_ab_wavefront_bands.jsonl)
+      W.bands = env_int("DRT_WAVEFRONT_BANDS", W.grid ? 1 : 8) >= 8 ? 8 : 1;
+      W.band = (W.n_slots + (uint32_t)W.bands - 1u) / (uint32_t)W.bands;
       launch_wf_gen(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
-      const uint64_t q = (uint64_t)(P.F.max_depth + 1) * (uint64_t)W.pairs * W.n_slots;
+      const uint64_t q = (uint64_t)W.levels * (uint64_t)W.pairs * W.band * (uint64_t)W.bands;
+      const uint32_t part_len = (uint32_t)((uint64_t)W.levels * W.pairs * W.band);
       unsigned int* counter = d_counter.as<unsigned int>() + 256u * (1u + k);
       if (q && W.grid) {
         // the Grid's shadow queries on its persistent stepper (MODE_QSTREAM): Grid::Traverse(Ray&)'s answer
@@ -1339,7 +1346,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         FrameArgs FQ = F2;
         FQ.mode = MODE_QSTREAM;
         FQ.n_items = q;
-        FQ.part_items = (uint32_t)((q + 7) / 8);
+        FQ.part_items = W.bands == 8 ? part_len : (uint32_t)((q + 7) / 8);
         FQ.q_rays = W.rays;
         FQ.q_occ = W.occ;
         FQ.work_counter = counter;
@@ -1359,6 +1366,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         // batched queries' 6 / 24 (8 / 16: 2 393-2 404, 7 / 8: 2 391-2 395; r05_wavefront_knobs_*.jsonl)
         A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 16);
         A.sparse = 1;
+        A.parts = W.bands;
+        A.part_len = W.bands == 8 ? part_len : (uint32_t)q;
         launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);
         DRT_HIP(c, hipGetLastError());
       }
@@ -1608,6 +1617,8 @@ static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, 
   A.occ_out = docc;
   A.stats = c->d_tstats.as<unsigned long long>();
   A.refill_min = env_int("DRT_TRACE_REFILL_MIN", 24);
+  A.parts = 1;
+  A.part_len = (uint32_t)n;
   DRT_HIP(c, hipEventRecord(c->tev[0], st));
   launch_trace_stream(S, A, shadow != 0, c->tri_only, stats, env_int("DRT_TRACE_WAVES", 6), st);
   DRT_HIP(c, hipGetLastError());

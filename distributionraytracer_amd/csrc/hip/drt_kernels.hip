@@ -2343,7 +2343,10 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
   // from that wave-private range: one counter word serves only ~90 dequeues/us
   // (MI355X_MICROARCH.md, dequeue), so a claim per refill would cap the kernel near 1 Gquery/s.
   uint32_t chunk_next = 0, chunk_end = 0;  // wave-uniform
-  bool exhausted = false;                  // wave-uniform: the counter is past the end
+  bool exhausted = false;                  // wave-uniform: every partition's counter is past its end
+  // partitions (TraceArgs::parts): a wave starts on its XCD's (HW_REG_XCC_ID), as path_persistent does
+  uint32_t part = A.parts > 1 ? (__builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u) % (uint32_t)A.parts : 0u;
+  uint32_t parts_done = 0;
   while (true) {
     const uint64_t idle = __ballot(L.item == kNoItem);
     const int n_idle = __popcll(idle);
@@ -2353,13 +2356,17 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
       uint64_t want = idle;
       int n_want = n_idle;
       while (true) {
-      if (chunk_next >= chunk_end && !exhausted) {
+      while (chunk_next >= chunk_end && !exhausted) {  // claim from the wave's current partition
+        const uint32_t pbeg = part * A.part_len, pend = min(pbeg + A.part_len, A.n);
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(A.counter, kTraceChunk);
-        base = __shfl(base, 0, 64);
+        if (lane == 0) base = atomicAdd(A.counter + 16u * part, kTraceChunk);
+        base = __shfl(base, 0, 64) + pbeg;
         chunk_next = base;
-        chunk_end = base < A.n ? min(base + kTraceChunk, A.n) : base;
-        if (base + kTraceChunk >= A.n) exhausted = true;
+        chunk_end = base < pend ? min(base + kTraceChunk, pend) : base;
+        if (base + kTraceChunk >= pend) {  // this partition is claimed: the next one
+          part = part + 1u == (uint32_t)A.parts ? 0u : part + 1u;
+          if (++parts_done == (uint32_t)A.parts) exhausted = true;
+        }
       }
       if (L.item == kNoItem) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -2445,13 +2452,23 @@ __device__ __forceinline__ bool wf_pair_used(const SceneArgs& S, const FrameArgs
   return m == 1 || j % m == 0 || S.lights[j / m].type == DRT_LIGHT_QUAD;
 }
 
+// Query slot of (level l, pair u, chunk slot s): [band][level][pair][slot in band], a band being W.band
+// consecutive sample slots, so that band b's queries are one contiguous range (the streaming kernels
+// give XCD b that range first: its L2 then serves the rays of one screen band)
+__device__ __forceinline__ size_t wf_q(const WfArgs& W, int l, int u, uint32_t s) {
+  const uint32_t b = s / W.band, o = s - b * W.band;
+  return (((size_t)b * (uint32_t)W.levels + (uint32_t)l) * (uint32_t)W.pairs + (uint32_t)u) * W.band + o;
+}
+
 __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // the slot's place in this chunk's buffers
-  if (slot >= W.n_slots) return;
+  if (slot >= W.band * (uint32_t)W.bands) return;
+  const bool in = slot < W.n_slots;  // (the last band's padding slots get empty queries only)
   const uint32_t g = W.slot0 + slot;  // the frame's sample slot
   const size_t ns = W.n_slots;
   const int md = F.max_depth, np = W.pairs;
-  const Item it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
+  Item it{0, 0, 0, false};
+  if (in) it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
   int l = 0;
   if (it.valid) {
     const uint32_t rec = F.chain_div > 1 ? (g - (uint32_t)it.sub) / (uint32_t)F.chain_div : g;
@@ -2502,7 +2519,7 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
       V3 lightPos = mk(0, 0, 0);
       for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // setup_shadow for every pair the light loop visits
         if (!wf_pair_used(S, F, j)) continue;
-        const size_t qi = ((size_t)l * np + u++) * ns + slot;
+        const size_t qi = wf_q(W, l, u++, slot);
         const int li = light_of_pair(j, F);
         lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
         V3 Lv = sub(lightPos, hitP);
@@ -2555,7 +2572,7 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
   }
   // no shadow query in the levels past the chain's end (a miss level has none either)
   for (int k = it.valid ? l : 0; k <= md; k++)
-    for (int j = 0; j < np; j++) W.rays[2 * (((size_t)k * np + j) * ns + slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    for (int j = 0; j < np; j++) W.rays[2 * wf_q(W, k, j, slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
 }
 
 __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
@@ -2587,7 +2604,7 @@ __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs 
     V3 acc = mk(0, 0, 0);
     for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // main.cpp:444-450, in the light loop's order
       if (!wf_pair_used(S, F, j)) continue;
-      const size_t qi = ((size_t)l * np + u++) * ns + slot;
+      const size_t qi = wf_q(W, l, u++, slot);
       if (W.occ[qi]) continue;
       const float2 nl = W.nl[qi];
       acc = add(acc, light_term(m, nl.x, nl.y, S.lights[light_of_pair(j, F)], F));
@@ -2606,7 +2623,8 @@ __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs 
 }
 
 void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {
-  hipLaunchKernelGGL(wf_gen_kernel, dim3((W.n_slots + 255) / 256), dim3(256), 0, st, S, F, W);
+  const uint32_t n = W.band * (uint32_t)W.bands;  // every band slot (padding included) gets its queries written
+  hipLaunchKernelGGL(wf_gen_kernel, dim3((n + 255) / 256), dim3(256), 0, st, S, F, W);
 }
 void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {
   hipLaunchKernelGGL(wf_combine_kernel, dim3((W.n_slots + 255) / 256), dim3(256), 0, st, S, F, W);

@@ -207,6 +207,9 @@ struct WfArgs {
   float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
   uint32_t n_slots;  // sample slots of this chunk of the frame (the buffers' slot dimension)
   uint32_t slot0;    // the chunk's first sample slot
+  uint32_t band;     // sample slots per band (wf_q); bands * band >= n_slots
+  int bands;
+  int levels;        // max_depth + 1
   int inorder;       // an in-order (DoF / glossy) frame: keyed-stream draws from FrameArgs::skel_rk (MODE_REPLAY)
   int grid;       // Grid scene: queries as Grid::Traverse(Ray&) takes them (unit L, range |L|)
   int pairs;      // query slots per level: the (light, k) pairs the light loop visits (a point light: k = 0 only)
@@ -223,6 +226,10 @@ struct TraceArgs {
   unsigned long long* stats;   // ST_* counters (stats launches only)
   int refill_min;
   int sparse;                  // shadow queries with thr < 0 are empty slots: skipped, occ_out not written
+  // work partitions: `parts` ranges of part_len queries, one claim counter each (64 B apart); a wave
+  // starts on the range of its XCD and moves on when that one is claimed (parts 1: one counter)
+  int parts;
+  uint32_t part_len;
 };
 
 struct ReduceArgs {

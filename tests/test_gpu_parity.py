@@ -943,7 +943,9 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
     ("grid", 9, "point", 4, 2, 0, 0), ("grid", 0, "quad", 1, 3, 0, 0),
     # in-order frames (glossy: MODE_SKEL + MODE_REPLAY's keyed-stream draws), and pass 2 in chunks
     ("bvh", 16, "quad", 1, 8, 0.1, 0), ("bvh", 0, "point", 1, 4, 0.2, 0), ("grid", 9, "quad", 1, 3, 0.2, 0),
-    ("bvh", 16, "quad", 4, 4, 0, 5000), ("bvh", 9, "point", 1, 6, 0.1, 7777), ("grid", 16, "quad", 1, 3, 0, 9000)])
+    ("bvh", 16, "quad", 4, 4, 0, 5000), ("bvh", 9, "point", 1, 6, 0.1, 7777), ("grid", 16, "quad", 1, 3, 0, 9000),
+    # XCD bands of the query array (DRT_WAVEFRONT_BANDS=8; chunk -1: bands alone)
+    ("bvh", 16, "point", 1, 4, 0, -1), ("grid", 9, "quad", 1, 3, 0.2, -1)])
 def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, accel, spp, first, light_spp, md, rough,
                                                    chunk):
     """Pass 2 of an AA / Whitted two-pass BVH frame as a wavefront (round 5; drt_kernels.hpp WfArgs):
@@ -953,10 +955,15 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, a
     reference-order frame bit for bit, with the same shadow rays and shadow-tree work — AA with a quad
     light first or last and 4 area samples per light, the depth cut at max_depth 1..8, Whitted frames,
     in-order (glossy) frames whose lens and reflectDir draws wf_gen takes from the recorded stream
-    positions, and pass 2 in chunks of sample slots (DRT_WAVEFRONT_CHUNK_SLOTS, a partial last chunk).
+    positions, pass 2 in chunks of sample slots (DRT_WAVEFRONT_CHUNK_SLOTS, a partial last chunk), and the
+    query array in 8 XCD bands (DRT_WAVEFRONT_BANDS, a padded last band).
     On the Grid the queries run on its persistent stepper (MODE_QSTREAM), with the same cell work."""
-    if chunk:
+    if chunk > 0:
         monkeypatch.setenv("DRT_WAVEFRONT_CHUNK_SLOTS", str(chunk))
+    # (BVH frames default to 8 XCD bands, Grid frames to 1): chunked frames run with 8, so the last band
+    # of a chunk is padded, and the other cases with the default
+    if chunk:
+        monkeypatch.setenv("DRT_WAVEFRONT_BANDS", "8")
     import bench
 
     s = drt.Scene()
