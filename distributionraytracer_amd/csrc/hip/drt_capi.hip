@@ -1303,6 +1303,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
           c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
         wavefront = true;
         W.rays = c->d_wf_rays_s[slot].as<float4>();
+        W.rays_b = W.rays + std::max<uint64_t>(q, 1);
         W.nl = c->d_wf_nl_s[slot].as<float2>();
         W.occ = c->d_wf_occ_s[slot].as<uint8_t>();
         W.lvl = c->d_wf_lvl_s[slot].as<float4>();
@@ -1348,6 +1349,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         FQ.n_items = q;
         FQ.part_items = W.bands == 8 ? part_len : (uint32_t)((q + 7) / 8);
         FQ.q_rays = W.rays;
+        FQ.q_rays_b = W.rays_b;
         FQ.q_occ = W.occ;
         FQ.work_counter = counter;
         FQ.process_min = 1;
@@ -1358,6 +1360,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       } else if (q) {
         TraceArgs A{};
         A.rays = W.rays;
+        A.rays_b = W.rays_b;
+        A.stride = 1;
         A.n = (uint32_t)q;
         A.counter = counter;
         A.occ_out = W.occ;
@@ -1610,6 +1614,8 @@ static int trace_device(drt_ctx* c, const float* d_rays, int32_t n, int shadow, 
   if (stats) DRT_HIP(c, hipMemsetAsync(c->d_tstats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
   TraceArgs A{};
   A.rays = q;
+  A.rays_b = q + 1;
+  A.stride = 2;
   A.n = (uint32_t)n;
   A.counter = c->d_counter.as<unsigned int>();
   A.t_out = dt;

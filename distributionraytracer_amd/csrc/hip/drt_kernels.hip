@@ -2019,12 +2019,12 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     return;
   }
   if (MODE == MODE_QSTREAM) {  // work item = one shadow query of a wavefront replay
-    const float4 a = F.q_rays[2 * (size_t)item];
+    const float4 a = F.q_rays[item];
     if (a.w < 0.0f) {  // an empty slot: no query
       L.item = kNoItem;
       return;
     }
-    const float4 b = F.q_rays[2 * (size_t)item + 1];
+    const float4 b = F.q_rays_b[item];
     L.fl = 0u;
     start_query<STATS, ACC>(S, L, make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)), true, a.w, C);
     return;
@@ -2372,9 +2372,11 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
         const uint32_t it = chunk_next + rank;
         if (it < chunk_end) {
-          const float4 a = A.rays[2 * (size_t)it];
+          // (interleaved records: rays_b = rays + 1, stride 2; or two arrays, stride 1)
+          const size_t at = (size_t)it * (uint32_t)A.stride;
+          const float4 a = A.rays[at];
           if (!A.sparse || a.w >= 0.0f) {
-          const float4 b = A.rays[2 * (size_t)it + 1];
+          const float4 b = A.rays_b[at];
           L.item = it;
           L.q = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
           L.thr = a.w;
@@ -2531,8 +2533,8 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
         // BVH::Traverse(Ray&) normalises Ls, range |Ls| + EPSILON; Grid::Traverse(Ray&) gets the unit L,
         // range |L|, direction re-normalised (Q1; setup_shadow)
         const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
-        W.rays[2 * qi] = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
-        W.rays[2 * qi + 1] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+        W.rays[qi] = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
+        W.rays_b[qi] = make_float4(sd.x, sd.y, sd.z, 0.0f);
         W.nl[qi] = make_float2(NdotL, NdotH);
       }
       uint32_t flags = 0u;
@@ -2572,7 +2574,7 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
   }
   // no shadow query in the levels past the chain's end (a miss level has none either)
   for (int k = it.valid ? l : 0; k <= md; k++)
-    for (int j = 0; j < np; j++) W.rays[2 * wf_q(W, k, j, slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    for (int j = 0; j < np; j++) W.rays[wf_q(W, k, j, slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
 }
 
 __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {

@@ -184,7 +184,8 @@ struct FrameArgs {
   // record index
   int tree_recs;
   // MODE_QSTREAM: 2 float4 per query ((o, range), (d, 0)), 1 byte per answer (1 = shadowed)
-  const float4* q_rays;
+  const float4* q_rays;    // per query: (o, range); thr < 0: no query
+  const float4* q_rays_b;  // per query: (d, 0)
   uint8_t* q_occ;
 };
 
@@ -201,7 +202,8 @@ constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 192;
 // walks the levels back, adding the unshadowed light terms in the reference's order, and writes the
 // sample.
 struct WfArgs {
-  float4* rays;   // 2 per query slot: (o, thr), (d, 0); thr < 0: no query in this slot
+  float4* rays;    // per query slot: (o, thr); thr < 0: no query in this slot
+  float4* rays_b;  // per query slot: (d, 0) — a second array, so that each store / load is one contiguous run
   float2* nl;     // per query slot: (NdotL, NdotH)
   uint8_t* occ;   // per query slot: 1 = occluded (trace_stream)
   float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
@@ -218,6 +220,8 @@ struct WfArgs {
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
 struct TraceArgs {
   const float4* rays;          // 2 per query: (o.xyz, range threshold), (d.xyz, 0); shadow d is unit
+  const float4* rays_b;        // query i: (o, range) at rays[i * stride], (d, 0) at rays_b[i * stride]
+  int stride;                  // 2: interleaved records (rays_b = rays + 1); 1: two arrays
   uint32_t n;
   unsigned int* counter;       // next unclaimed query (zeroed per launch)
   float* t_out;                // closest: best t (FLT_MAX on a miss)

@@ -945,7 +945,9 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
     ("bvh", 16, "quad", 1, 8, 0.1, 0), ("bvh", 0, "point", 1, 4, 0.2, 0), ("grid", 9, "quad", 1, 3, 0.2, 0),
     ("bvh", 16, "quad", 4, 4, 0, 5000), ("bvh", 9, "point", 1, 6, 0.1, 7777), ("grid", 16, "quad", 1, 3, 0, 9000),
     # XCD bands of the query array (DRT_WAVEFRONT_BANDS=8; chunk -1: bands alone)
-    ("bvh", 16, "point", 1, 4, 0, -1), ("grid", 9, "quad", 1, 3, 0.2, -1)])
+    ("bvh", 16, "point", 1, 4, 0, -1), ("grid", 9, "quad", 1, 3, 0.2, -1),
+    # a scene without lights: no shadow query at all, the frame is the mirrored background
+    ("bvh", 16, "none", 1, 4, 0, 0), ("grid", 4, "none", 1, 2, 0, 0)])
 def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, accel, spp, first, light_spp, md, rough,
                                                    chunk):
     """Pass 2 of an AA / Whitted two-pass BVH frame as a wavefront (round 5; drt_kernels.hpp WfArgs):
@@ -976,7 +978,7 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, a
     if first == "quad":
         s.add_light_quad(*quad)
         s.add_light_point((-3, 1, 5), (1, 1, 1))
-    else:
+    elif first == "point":
         s.add_light_point((-3, 1, 5), (1, 1, 1))
         s.add_light_quad(*quad)
     s.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), 0.5, 30.0827, 0, 1)
@@ -997,7 +999,8 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, a
     np.testing.assert_array_equal(bits(wf), bits(pers))
     np.testing.assert_array_equal(bits(wf), bits(ref))
     assert st["samples"] == st1["samples"] == rst["samples"]
-    assert st["shadow_rays"] == st1["shadow_rays"] == rst["shadow_rays"] > 0
+    assert st["shadow_rays"] == st1["shadow_rays"] == rst["shadow_rays"]
+    assert (st["shadow_rays"] > 0) == (first != "none")
     for k in ("closest_rays", "closest_inner", "closest_leaf", "closest_prims", "shadow_inner", "shadow_leaf",
               "shadow_prims"):
         assert st[k] == st1[k], k
