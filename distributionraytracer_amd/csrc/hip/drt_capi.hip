@@ -1353,7 +1353,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         FQ.q_occ = W.occ;
         FQ.work_counter = counter;
         FQ.process_min = 1;
-        FQ.refill_min = env_int("DRT_WAVEFRONT_GRID_REFILL_MIN", P.F.refill_min);
+        // refill at 16 idle lanes: 1 875 against 1 758 Mrays/s at the path kernel's 8 (24: 1 874-1 878,
+        // 32: 1 809, 4: 1 576; profiles/r05_grid_qstream_knobs*.jsonl)
+        FQ.refill_min = env_int("DRT_WAVEFRONT_GRID_REFILL_MIN", 16);
         FQ.waves = env_int("DRT_WAVEFRONT_GRID_WAVES", 5);
         launch_path_persistent(S, FQ, c->accel, c->tri_only, stats, st);
         DRT_HIP(c, hipGetLastError());

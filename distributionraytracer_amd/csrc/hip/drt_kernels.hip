@@ -2158,6 +2158,9 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         if (base + rank < pn) lane_init<STATS, MODE, ACC>(S, F, L, pbeg + base + rank, C);
       }
+      // (Measured alternative, kept out: MODE_QSTREAM lanes that drew an empty slot claiming again, up to
+      // three times, while refill_min lanes are idle — 1 863-1 869 against 1 868-1 875 Mrays/s on the Grid
+      // headline at refill 16, profiles/r05_grid_qstream_reclaim_ab.jsonl.)
     }
     if (MODE == MODE_SEQ && exhausted && F.seq_cont && part != kPartYield) {
       const uint64_t idle2 = __ballot(L.item == kNoItem);
