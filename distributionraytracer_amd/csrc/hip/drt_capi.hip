@@ -1260,6 +1260,31 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   if (P.F.n_items && P.two_pass) {
     DevBuf& d_rk = c->d_skel_rk_s[slot];  // allocated above
     DevBuf& d_hits = c->d_skel_hits_s[slot];
+    // pass 2 as a wavefront (plan_frame): the query buffers, or the persistent replay if they do not fit
+    bool wavefront = false;
+    WfArgs W{};
+    if (P.wavefront) {
+      const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
+      const uint64_t q = levels * pairs * (P.wf_chunk + 8u);  // (+ the last band's padding, wf_q)
+      if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
+        wavefront = true;
+        W.rays = c->d_wf_rays_s[slot].as<float4>();
+        W.rays_b = W.rays + std::max<uint64_t>(q, 1);
+        W.nl = c->d_wf_nl_s[slot].as<float2>();
+        W.occ = c->d_wf_occ_s[slot].as<uint8_t>();
+        W.lvl = c->d_wf_lvl_s[slot].as<float4>();
+        W.pairs = (int)pairs;
+        W.levels = (int)levels;
+        W.grid = c->accel == DRT_ACCEL_GRID ? 1 : 0;
+        W.inorder = P.aa_chain ? 0 : 1;
+      } else {
+        (void)hipGetLastError();
+        for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot]}) b->release();
+      }
+    }
     FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order (AA: any order)
     F1.mode = P.tree ? MODE_TCHAIN : (P.aa_chain ? MODE_CHAIN : MODE_SKEL);
     F1.tree_recs = (int)P.recs;
@@ -1288,34 +1313,13 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       F1.process_min = env_int("DRT_SKEL_PROCESS_MIN", P.F.process_min);
     }
     F1.seq_cont = nullptr;
+    // (Measured alternative, kept out: the AA closest-chain pass writing each level's shadow queries and
+    // record itself instead of wf_gen reading the hits back — its code in the chain loop cost 14 VGPR
+    // spills, 2 339 against 2 380 Mrays/s fused / unfused in that build and 2 475 without it;
+    // profiles/r05_ab_fused_chain_gen.jsonl.)
     launch_path_persistent(S, F1, c->accel, c->tri_only, stats, st);
     DRT_HIP(c, hipGetLastError());
     DRT_HIP(c, hipEventRecord(ev[3], st));  // end of pass 1 (drt_frame_pass_times)
-    // pass 2 as a wavefront (plan_frame): the query buffers, or the persistent replay if they do not fit
-    bool wavefront = false;
-    WfArgs W{};
-    if (P.wavefront) {
-      const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
-      const uint64_t q = levels * pairs * (P.wf_chunk + 8u);  // (+ the last band's padding, wf_q)
-      if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
-        wavefront = true;
-        W.rays = c->d_wf_rays_s[slot].as<float4>();
-        W.rays_b = W.rays + std::max<uint64_t>(q, 1);
-        W.nl = c->d_wf_nl_s[slot].as<float2>();
-        W.occ = c->d_wf_occ_s[slot].as<uint8_t>();
-        W.lvl = c->d_wf_lvl_s[slot].as<float4>();
-        W.pairs = (int)pairs;
-        W.levels = (int)levels;
-        W.grid = c->accel == DRT_ACCEL_GRID ? 1 : 0;
-        W.inorder = P.aa_chain ? 0 : 1;
-      } else {
-        (void)hipGetLastError();
-        for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot]}) b->release();
-      }
-    }
     FrameArgs F2 = F1;  // pass 2: every sample on its own, closest hits read back
     F2.mode = P.tree ? MODE_TREPLAY : (P.aa_chain ? MODE_AREPLAY : MODE_REPLAY);
     F2.heads = (!P.aa_chain && c->accel == DRT_ACCEL_BVH) ? c->d_heads_s[slot].as<float4>() : nullptr;

@@ -1878,6 +1878,104 @@ again:  // (A/B) the replay pass shades a read-back closest hit at once instead 
   finish_sample<STATS, MODE, ACC>(S, F, L, C, c);
 }
 
+// ------------------------------------------------------------------------------------------
+// Wavefront replay (round 5; drt_kernels.hpp WfArgs): pass 2 of a refraction-free two-pass frame as
+// three launches — wf_gen, the shadow queries of the whole frame on the streaming kernel, wf_combine —
+// instead of the persistent replay, whose waves interleave shading (a third of their lanes active) with
+// the shadow traversal.  The arithmetic is lane_process's, in its order: setup_shadow's light point, ray
+// and Phong factors per (level, light pair), the unshadowed terms added in pair order, the depth cut,
+// and the mirror unwind.
+// ------------------------------------------------------------------------------------------
+enum : uint32_t { WF_MISS = 1u, WF_DEEP = 2u, WF_REFL = 4u, WF_RN = 8u, WF_KR1 = 16u };
+
+__device__ __forceinline__ bool wf_pair_used(const SceneArgs& S, const FrameArgs& F, int j) {
+  // the pairs next_light_pair visits: every quad-light pair, a point light's k = 0 only
+  const int m = F.light_spp;
+  return m == 1 || j % m == 0 || S.lights[j / m].type == DRT_LIGHT_QUAD;
+}
+
+// Query slot of (level l, pair u, chunk slot s): [band][level][pair][slot in band], a band being W.band
+// consecutive sample slots, so that band b's queries are one contiguous range (the streaming kernels
+// give XCD b that range first: its L2 then serves the rays of one screen band)
+__device__ __forceinline__ size_t wf_q(const WfArgs& W, int l, int u, uint32_t s) {
+  const uint32_t b = s / W.band, o = s - b * W.band;
+  return (((size_t)b * (uint32_t)W.levels + (uint32_t)l) * (uint32_t)W.pairs + (uint32_t)u) * W.band + o;
+}
+
+// One level of a sample's recorded chain (wf_gen_kernel): a miss's background colour, or the hit's shadow queries — one per pair
+// the light loop visits, with their Phong factors — and the level record (material, flags).  Returns
+// whether the sample goes on with its mirror ray `next`; `ls` becomes the light sample it carries.
+__device__ bool wf_level(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, uint32_t slot, int l, const RayP& q,
+                         bool hit, float t, uint32_t prim, V3& ls, uint32_t pmix, uint32_t& rk, RayP& next) {
+  const size_t li_ = (size_t)l * W.n_slots + slot;
+  if (!hit) {  // main.cpp:351-357
+    const V3 c = cclamp(background(S, q.d));
+    W.lvl[li_] = make_float4(c.x, c.y, c.z, __uint_as_float(WF_MISS << 24));
+    return false;
+  }
+  const V3 hitP = add(q.o, mul(q.d, t));
+  V3 N = normalize(prim_normal(S.prims, prim, q, t));
+  const bool outside = dot(q.d, N) < 0.0f;
+  if (!outside) N = neg(N);
+  const uint32_t mat = prim_material(S.prims[3 * prim]);
+  const V3 V = neg(normalize(q.d));
+  V3 lightPos = mk(0, 0, 0);
+  for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // setup_shadow for every pair the light loop visits
+    if (!wf_pair_used(S, F, j)) continue;
+    const size_t qi = wf_q(W, l, u++, slot);
+    const int li = light_of_pair(j, F);
+    lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
+    V3 Lv = sub(lightPos, hitP);
+    const V3 Ls = Lv;
+    Lv = normalize(Lv);
+    const V3 H = normalize(add(Lv, V));
+    const float NdotL = smax(dot(N, Lv), 0.0f), NdotH = smax(dot(N, H), 0.0f);
+    const V3 so = add(hitP, mul(N, 1e-4f));
+    // BVH::Traverse(Ray&) normalises Ls, range |Ls| + EPSILON; Grid::Traverse(Ray&) gets the unit L,
+    // range |L|, direction re-normalised (Q1; setup_shadow)
+    const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
+    W.rays[qi] = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
+    W.rays_b[qi] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+    W.nl[qi] = make_float2(NdotL, NdotH);
+  }
+  uint32_t flags = 0u;
+  bool more = false;
+  if (l + 1 > F.max_depth) {  // depth > MAX_DEPTH: the accumulated colour, unclamped (main.cpp:454)
+    flags = WF_DEEP;
+  } else {
+    const drt_material m = S.mats[mat];
+    float kr = m.refl;
+    float ior2 = m.ior;
+    if (!outside) ior2 = 1.0f;
+    const float eta = 1.0f / ior2;  // ior1: mirror children keep the camera's 1.0
+    const V3 Vt = sub(mul(N, dot(V, N)), V);
+    const float sin_t = eta * length(Vt);
+    if (m.trans > 0.0f && sin_t >= 1.0f) kr = 1.0f;  // (trans == 1 never reaches a two-pass frame)
+    if (m.ks > 0.0f) {  // reflectDir (reflect_dir)
+      V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
+      if (W.inorder) {
+        KRng rng{F.seed, pmix, rk};
+        R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
+        rk = rng.k;
+      } else {
+        R = normalize(R);
+      }
+      flags = WF_REFL | (dot(R, N) > 0.0f ? WF_RN : 0u) | (kr == 1.0f && m.refl != 1.0f ? WF_KR1 : 0u);
+      next = make_ray(add(hitP, mul(N, 1e-4f)), R);
+      ls = lightPos;
+      more = true;
+    }
+  }
+  W.lvl[li_] = make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24)));
+  return more;
+}
+// No shadow query at levels from..max_depth of chunk slot `slot` (past its chain's end; a miss level
+// has none either).
+__device__ __forceinline__ void wf_mark_empty(const WfArgs& W, int from, uint32_t slot) {
+  for (int k = from; k < W.levels; k++)
+    for (int j = 0; j < W.pairs; j++) W.rays[wf_q(W, k, j, slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+}
+
 // MODE_SKEL: the closest query of bounce L.depth of sample L.smp returned: record it.  A hit that
 // rayTracing() reflects from (depth <= MAX_DEPTH and Ks > 0, main.cpp:453-512; a two-pass scene has
 // no refraction) starts the mirror child with the sample's reflectDir draw, computed exactly as
@@ -2449,32 +2547,15 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
 // setup_shadow's light point, ray and Phong factors per (level, light pair), the unshadowed terms added
 // in pair order, the depth cut, and the mirror unwind.
 // ------------------------------------------------------------------------------------------
-enum : uint32_t { WF_MISS = 1u, WF_DEEP = 2u, WF_REFL = 4u, WF_RN = 8u, WF_KR1 = 16u };
-
-__device__ __forceinline__ bool wf_pair_used(const SceneArgs& S, const FrameArgs& F, int j) {
-  // the pairs next_light_pair visits: every quad-light pair, a point light's k = 0 only
-  const int m = F.light_spp;
-  return m == 1 || j % m == 0 || S.lights[j / m].type == DRT_LIGHT_QUAD;
-}
-
-// Query slot of (level l, pair u, chunk slot s): [band][level][pair][slot in band], a band being W.band
-// consecutive sample slots, so that band b's queries are one contiguous range (the streaming kernels
-// give XCD b that range first: its L2 then serves the rays of one screen band)
-__device__ __forceinline__ size_t wf_q(const WfArgs& W, int l, int u, uint32_t s) {
-  const uint32_t b = s / W.band, o = s - b * W.band;
-  return (((size_t)b * (uint32_t)W.levels + (uint32_t)l) * (uint32_t)W.pairs + (uint32_t)u) * W.band + o;
-}
-
 __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // the slot's place in this chunk's buffers
   if (slot >= W.band * (uint32_t)W.bands) return;
   const bool in = slot < W.n_slots;  // (the last band's padding slots get empty queries only)
   const uint32_t g = W.slot0 + slot;  // the frame's sample slot
-  const size_t ns = W.n_slots;
-  const int md = F.max_depth, np = W.pairs;
+  const int md = F.max_depth;
   Item it{0, 0, 0, false};
   if (in) it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
-  int l = 0;
+  int l = 0;  // the first level without shadow queries
   if (it.valid) {
     const uint32_t rec = F.chain_div > 1 ? (g - (uint32_t)it.sub) / (uint32_t)F.chain_div : g;
     const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
@@ -2505,79 +2586,17 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
                            ((float)(sb / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
                       : mk(0.5f, 0.5f, 0.0f);
     }
-    for (; l <= md; l++) {
+    while (l <= md) {
       const uint2 h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)l];
-      const size_t li_ = (size_t)l * ns + slot;
-      if (h.y == 0xFFFFFFFFu) {  // main.cpp:351-357
-        const V3 c = cclamp(background(S, q.d));
-        W.lvl[li_] = make_float4(c.x, c.y, c.z, __uint_as_float(WF_MISS << 24));
-        break;
-      }
-      const float t = __uint_as_float(h.x);
-      const uint32_t prim = h.y;
-      const V3 hitP = add(q.o, mul(q.d, t));
-      V3 N = normalize(prim_normal(S.prims, prim, q, t));
-      const bool outside = dot(q.d, N) < 0.0f;
-      if (!outside) N = neg(N);
-      const uint32_t mat = prim_material(S.prims[3 * prim]);
-      const V3 V = neg(normalize(q.d));
-      V3 lightPos = mk(0, 0, 0);
-      for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // setup_shadow for every pair the light loop visits
-        if (!wf_pair_used(S, F, j)) continue;
-        const size_t qi = wf_q(W, l, u++, slot);
-        const int li = light_of_pair(j, F);
-        lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
-        V3 Lv = sub(lightPos, hitP);
-        const V3 Ls = Lv;
-        Lv = normalize(Lv);
-        const V3 H = normalize(add(Lv, V));
-        const float NdotL = smax(dot(N, Lv), 0.0f), NdotH = smax(dot(N, H), 0.0f);
-        const V3 so = add(hitP, mul(N, 1e-4f));
-        // BVH::Traverse(Ray&) normalises Ls, range |Ls| + EPSILON; Grid::Traverse(Ray&) gets the unit L,
-        // range |L|, direction re-normalised (Q1; setup_shadow)
-        const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
-        W.rays[qi] = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
-        W.rays_b[qi] = make_float4(sd.x, sd.y, sd.z, 0.0f);
-        W.nl[qi] = make_float2(NdotL, NdotH);
-      }
-      uint32_t flags = 0u;
-      bool more = false;
-      if (l + 1 > md) {  // depth > MAX_DEPTH: the accumulated colour, unclamped (main.cpp:454)
-        flags = WF_DEEP;
-      } else {
-        const drt_material m = S.mats[mat];
-        float kr = m.refl;
-        float ior2 = m.ior;
-        if (!outside) ior2 = 1.0f;
-        const float eta = 1.0f / ior2;  // ior1: mirror children keep the camera's 1.0
-        const V3 Vt = sub(mul(N, dot(V, N)), V);
-        const float sin_t = eta * length(Vt);
-        if (m.trans > 0.0f && sin_t >= 1.0f) kr = 1.0f;  // (trans == 1 never reaches a two-pass frame)
-        if (m.ks > 0.0f) {  // reflectDir (reflect_dir)
-          V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
-          if (W.inorder) {
-            KRng rng{F.seed, pmix, rk};
-            R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
-            rk = rng.k;
-          } else {
-            R = normalize(R);
-          }
-          flags = WF_REFL | (dot(R, N) > 0.0f ? WF_RN : 0u) | (kr == 1.0f && m.refl != 1.0f ? WF_KR1 : 0u);
-          q = make_ray(add(hitP, mul(N, 1e-4f)), R);
-          ls = lightPos;
-          more = true;
-        }
-      }
-      W.lvl[li_] = make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24)));
-      if (!more) {
-        l++;
-        break;
-      }
+      const bool hit = h.y != 0xFFFFFFFFu;
+      RayP next;
+      const bool more = wf_level(S, F, W, slot, l, q, hit, __uint_as_float(h.x), h.y, ls, pmix, rk, next);
+      if (hit) l++;  // level l holds shadow queries
+      if (!more) break;
+      q = next;
     }
   }
-  // no shadow query in the levels past the chain's end (a miss level has none either)
-  for (int k = it.valid ? l : 0; k <= md; k++)
-    for (int j = 0; j < np; j++) W.rays[wf_q(W, k, j, slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+  wf_mark_empty(W, l, slot);
 }
 
 __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {

@@ -128,6 +128,29 @@ struct SceneArgs {
   uint32_t wroot;       // the root's wide record
 };
 
+// Wavefront replay of an AA / Whitted two-pass BVH frame without refraction (round 5): the closest hits
+// are all known after MODE_CHAIN, so every shading decision except occlusion is a function of them.
+// wf_gen (one thread per sample slot) walks each sample's recorded chain and writes every shadow query
+// of every level ([level][visited light pair][slot]: 32-B trace_stream records, thr < 0 = no query) with its
+// NdotL / NdotH, and one 16-B record per level; trace_stream answers the shadow queries; wf_combine
+// walks the levels back, adding the unshadowed light terms in the reference's order, and writes the
+// sample.
+struct WfArgs {
+  float4* rays;    // per query slot: (o, thr); thr < 0: no query in this slot
+  float4* rays_b;  // per query slot: (d, 0) — a second array, so that each store / load is one contiguous run
+  float2* nl;     // per query slot: (NdotL, NdotH)
+  uint8_t* occ;   // per query slot: 1 = occluded (trace_stream)
+  float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
+  uint32_t n_slots;  // sample slots of this chunk of the frame (the buffers' slot dimension)
+  uint32_t slot0;    // the chunk's first sample slot
+  uint32_t band;     // sample slots per band (wf_q); bands * band >= n_slots
+  int bands;
+  int levels;        // max_depth + 1
+  int inorder;       // an in-order (DoF / glossy) frame: keyed-stream draws from FrameArgs::skel_rk (MODE_REPLAY)
+  int grid;       // Grid scene: queries as Grid::Traverse(Ray&) takes them (unit L, range |L|)
+  int pairs;      // query slots per level: the (light, k) pairs the light loop visits (a point light: k = 0 only)
+};
+
 struct FrameArgs {
   uint32_t seed;
   int max_depth;
@@ -194,28 +217,6 @@ struct FrameArgs {
 // 64-bit pair, and the pixels finished, on a 128-B line of its own (every pixel adds to it).
 constexpr uint32_t kSeqPush = 128, kSeqPop = 129, kSeqDone = 192;
 
-// Wavefront replay of an AA / Whitted two-pass BVH frame without refraction (round 5): the closest hits
-// are all known after MODE_CHAIN, so every shading decision except occlusion is a function of them.
-// wf_gen (one thread per sample slot) walks each sample's recorded chain and writes every shadow query
-// of every level ([level][visited light pair][slot]: 32-B trace_stream records, thr < 0 = no query) with its
-// NdotL / NdotH, and one 16-B record per level; trace_stream answers the shadow queries; wf_combine
-// walks the levels back, adding the unshadowed light terms in the reference's order, and writes the
-// sample.
-struct WfArgs {
-  float4* rays;    // per query slot: (o, thr); thr < 0: no query in this slot
-  float4* rays_b;  // per query slot: (d, 0) — a second array, so that each store / load is one contiguous run
-  float2* nl;     // per query slot: (NdotL, NdotH)
-  uint8_t* occ;   // per query slot: 1 = occluded (trace_stream)
-  float4* lvl;    // per (level, slot): (background colour of a miss, material | flags << 24)
-  uint32_t n_slots;  // sample slots of this chunk of the frame (the buffers' slot dimension)
-  uint32_t slot0;    // the chunk's first sample slot
-  uint32_t band;     // sample slots per band (wf_q); bands * band >= n_slots
-  int bands;
-  int levels;        // max_depth + 1
-  int inorder;       // an in-order (DoF / glossy) frame: keyed-stream draws from FrameArgs::skel_rk (MODE_REPLAY)
-  int grid;       // Grid scene: queries as Grid::Traverse(Ray&) takes them (unit L, range |L|)
-  int pairs;      // query slots per level: the (light, k) pairs the light loop visits (a point light: k = 0 only)
-};
 
 // Streaming BVH traversal (trace_stream): one query per lane, refilled from a query array.
 struct TraceArgs {
