@@ -1372,9 +1372,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         A.counter = counter;
         A.occ_out = W.occ;
         A.stats = F2.stats;
-        // 7 waves / SIMD and refill at 16 idle lanes: 2 407 Mrays/s on the headline against 2 235 at the
-        // batched queries' 6 / 24 (8 / 16: 2 393-2 404, 7 / 8: 2 391-2 395; r05_wavefront_knobs_*.jsonl)
-        A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 16);
+        // 7 waves / SIMD and refill at 12 idle lanes: 2 487-2 491 Mrays/s on the headline against 2 235 at
+        // the batched queries' 6 / 24 (7 / 16: 2 475-2 480, 7 / 10: 2 479-2 489, 8 / 16: 2 393-2 400,
+        // 6 / 16: 2 431; C3 at 12 / 16: 3 430 / 3 425-3 427; r05_wavefront_knobs_*.jsonl)
+        A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 12);
         A.sparse = 1;
         A.parts = W.bands;
         A.part_len = W.bands == 8 ? part_len : (uint32_t)q;
