@@ -1201,7 +1201,12 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // in-range primitive hit becomes LF_VERIFY: the next step loads that primitive's exact reference
 // leaf box through the same shared loads and accepts the hit only if the box is hit
 // (boundingBox.cpp:64-124), else the leaf is dropped and the walk goes on.
-template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, int LEAF1 = 1, bool WIDE = false, class LaneT>
+// UNI (the streaming kernel's shadow queries): when the visiting lanes' record is the first visiting
+// lane's — a wave's queries come from consecutive samples of one pixel toward one light point, so their
+// walks coincide for long stretches — those lanes read it through one scalar load (the scalar cache)
+// instead of per-lane vector loads on the vector-memory path the kernel is bound by.
+template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, int LEAF1 = 1, bool WIDE = false, bool UNI = false,
+          class LaneT>
 __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kRowBytes;  // desc part; the t part follows
@@ -1226,7 +1231,25 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   const float4* rec = leaf ? S.prims + 3 * (size_t)first
                            : (verify ? S.wleaf + 2 * (size_t)cur : (wide ? S.wnodes : S.nodes) + 4 * (size_t)cur);
   float4 s0, s1, s2, s3, s4, s5;
-  if (visit) {
+  bool uni_done = false;
+  if (UNI && visit) {
+    const uint64_t ra = (uint64_t)(uintptr_t)rec;
+    const uint64_t r0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ra >> 32)) << 32) |
+                        (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ra);
+    if (ra == r0) {  // the first visiting lane's record: one scalar 64-B load serves these lanes
+      typedef const __attribute__((address_space(4))) uint32_t CU;
+      CU* p = (CU*)(const void*)(uintptr_t)r0;
+      uint32_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) w[k] = p[k];
+      __builtin_memcpy(&s0, w, 16);
+      __builtin_memcpy(&s1, w + 4, 16);
+      __builtin_memcpy(&s2, w + 8, 16);
+      __builtin_memcpy(&s3, w + 12, 16);
+      uni_done = true;
+    }
+  }
+  if (visit && !uni_done) {
     s0 = rec[0];
     s1 = rec[1];
     s2 = rec[2];
@@ -2418,6 +2441,17 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
 // state, holds 6.  The node step is the path kernel's, specialised for one query kind.
 // ------------------------------------------------------------------------------------------
 constexpr uint32_t kTraceChunk = 256;  // queries claimed per wave per atomic
+// shadow-query records through the scalar cache when a wave's visiting lanes share one (node_step UNI;
+// -DDRT_UNI_FETCH, A/B): measured 2 418-2 447 against 2 487-2 495 Mrays/s on the headline and 3 284-3 356
+// against 3 421-3 442 on C3 (profiles/r05_ab_uniform_node_fetch.jsonl) — the lanes of a wave leave a
+// shared walk within a few steps, and the per-step readfirstlane / compare / divergent scalar path costs
+// more than the vector loads it saves.  Off.
+constexpr bool kUniFetch =
+#ifdef DRT_UNI_FETCH
+    true;
+#else
+    false;
+#endif
 
 struct TLane {
   uint32_t item, fl;
@@ -2514,7 +2548,8 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
       // one primitive of a leaf per step in triangle scenes only, as in the path kernel (mixed-primitive
       // scenes measured ~10 % slower with it there)
       if (in_trav)
-        node_step<TRI_ONLY, STATS, CAP, KIND, TRI_ONLY ? 1 : 0, KIND == 2>(S, L, (LdsByte*)lds_bytes, ov_desc, ov_t,
+        node_step<TRI_ONLY, STATS, CAP, KIND, TRI_ONLY ? 1 : 0, KIND == 2, kUniFetch && KIND == 2>(
+            S, L, (LdsByte*)lds_bytes, ov_desc, ov_t,
                                                                             wave_finite, C, cyc_leaf);
     }
     if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
