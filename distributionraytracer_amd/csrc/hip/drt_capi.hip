@@ -1302,7 +1302,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       // measured 1 927 against 1 897 Mrays/s for 24 (1: 1 842, 48: 1 725; profiles/r04_pass_knobs_ab.jsonl)
       // (Grid: 5 waves, 1 381 against 1 318 Mrays/s at 6 on the Grid headline scene;
       // profiles/r04_grid_two_pass_wide_order_ab.jsonl)
-      F1.waves = env_int("DRT_CHAIN_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 6);  // BVH: 7 measured 1 785
+      // (BVH: 7 waves since round 5 — the chain pass has its own instantiation and no spills at 6 since
+      // MODE_AREPLAY split off: 2 534-2 545 against 2 483-2 488 Mrays/s, C3 3 471-3 473 against 3 425;
+      // round 4 measured 1 785 against 1 897 at 7; profiles/r05_chain_knobs.jsonl)
+      F1.waves = env_int("DRT_CHAIN_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 7);
       F1.process_min = env_int("DRT_CHAIN_PROCESS_MIN", 8);
       F1.refill_min = env_int("DRT_CHAIN_REFILL_MIN", P.F.refill_min);  // 16 measured 1 868
       // Grid: 3 empty cells per call in both passes of an AA two-pass frame (1 420 against 1 383 Mrays/s

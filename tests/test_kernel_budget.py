@@ -36,6 +36,8 @@ BUDGET = {
     # round 4: the headline's AA frame in two passes — its closest-chain pass, and (round 5: its own
     # instantiation, MODE_AREPLAY, no RNG code: 45 -> 35 spills) its replay pass
     "drt::path_persistent<true, false, 7, 6, 2>": (80, 704, 6, 2),
+    # (round 5: the AA closest-chain pass runs at 7 waves/SIMD by default)
+    "drt::path_persistent<true, false, 7, 7, 2>": (72, 736, 7, 8),
     "drt::path_persistent<true, false, 8, 6, 2>": (80, 2224, 6, 42),
     # batched shadow queries (drt_trace_shadow) on the 4-ary shadow tree: 8 waves/SIMD, no spills
     # (round 5: 64 VGPRs with the two-array query records (TraceArgs::stride): 7 waves by the compiler's
