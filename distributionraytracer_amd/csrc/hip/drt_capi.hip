@@ -1302,10 +1302,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       // measured 1 927 against 1 897 Mrays/s for 24 (1: 1 842, 48: 1 725; profiles/r04_pass_knobs_ab.jsonl)
       // (Grid: 5 waves, 1 381 against 1 318 Mrays/s at 6 on the Grid headline scene;
       // profiles/r04_grid_two_pass_wide_order_ab.jsonl)
-      // (BVH: 7 waves since round 5 — the chain pass has its own instantiation and no spills at 6 since
-      // MODE_AREPLAY split off: 2 534-2 545 against 2 483-2 488 Mrays/s, C3 3 471-3 473 against 3 425;
-      // round 4 measured 1 785 against 1 897 at 7; profiles/r05_chain_knobs.jsonl)
-      F1.waves = env_int("DRT_CHAIN_WAVES", c->accel == DRT_ACCEL_GRID ? 5 : 7);
+      // (7 waves since round 5 — the chain pass has its own instantiation and no spills at 6 since
+      // MODE_AREPLAY split off: BVH 2 534-2 545 against 2 483-2 488 Mrays/s, C3 3 471-3 473 against 3 425;
+      // Grid 1 963-1 967 against 1 872-1 876 at 5 (6: 1 930); round 4 measured 1 785 against 1 897 at 7 on
+      // the BVH; profiles/r05_chain_knobs.jsonl, r05_grid_waves.jsonl)
+      F1.waves = env_int("DRT_CHAIN_WAVES", 7);
       F1.process_min = env_int("DRT_CHAIN_PROCESS_MIN", 8);
       F1.refill_min = env_int("DRT_CHAIN_REFILL_MIN", P.F.refill_min);  // 16 measured 1 868
       // Grid: 3 empty cells per call in both passes of an AA two-pass frame (1 420 against 1 383 Mrays/s
@@ -1363,7 +1364,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         // refill at 16 idle lanes: 1 875 against 1 758 Mrays/s at the path kernel's 8 (24: 1 874-1 878,
         // 32: 1 809, 4: 1 576; profiles/r05_grid_qstream_knobs*.jsonl)
         FQ.refill_min = env_int("DRT_WAVEFRONT_GRID_REFILL_MIN", 16);
-        FQ.waves = env_int("DRT_WAVEFRONT_GRID_WAVES", 5);
+        FQ.waves = env_int("DRT_WAVEFRONT_GRID_WAVES", 7);  // 7: +0.7 % against 5 (r05_grid_waves.jsonl)
         launch_path_persistent(S, FQ, c->accel, c->tri_only, stats, st);
         DRT_HIP(c, hipGetLastError());
       } else if (q) {

@@ -2864,7 +2864,8 @@ static void launch_persistent_m(const SceneArgs& S, const FrameArgs& F, hipStrea
   if (A == ACC_GRID) {
     // (the Grid's closest-chain pass: 5 waves; 4 measured 1 364-1 369 against 1 424-1 427 Mrays/s,
     // 6 measured 1 318 against 1 381, profiles/r04_grid_chain_waves_ab.jsonl)
-    if (F.waves == 6) launch_persistent_w<T, ST, M, 6, A>(S, F, st);
+    if (F.waves == 7) launch_persistent_w<T, ST, M, 7, A>(S, F, st);
+    else if (F.waves == 6) launch_persistent_w<T, ST, M, 6, A>(S, F, st);
     else launch_persistent_w<T, ST, M, 5, A>(S, F, st);
     return;
   }
