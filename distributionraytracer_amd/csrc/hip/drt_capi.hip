@@ -1048,11 +1048,19 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // (BVH) or the Grid.  Same conditions as the AA frames'; a quad-light frame of >= 4 light samples
   // at any size (the closest work shrinks grid_res times), a point-light frame by the AA size rule.
   // DRT_WHITTED_TWO_PASS=0 keeps one pass.
+  // A Grid scene of mixed primitives without a refracting material takes two passes at any size: its
+  // one-pass kernel is the mixed-primitive Grid stepper at 5 waves/SIMD (79 VGPR spills), while the
+  // chain pass and the wavefront's shadow stream run at 7 — the shipped balls_high Whitted frame (7 383
+  // spheres, point light) 3.48 -> 2.05 ms at 512^2 and 4.87 -> 3.76 ms at 1024^2, where the triangle
+  // scenes' point-light frames (dragon) and the glass scene's tree frames (assignment1) measured 8-50 %
+  // slower in two passes (profiles/r05_whitted_two_pass_wavefront.jsonl).
   P.chain_div = 1;
   const bool whitted = F.mode == MODE_WHITTED_QUAD || F.mode == MODE_WHITTED_POINT;
+  bool grid_mixed = grid_chain && !c->tri_only;
+  for (const drt_material& m : c->mats) grid_mixed = grid_mixed && m.trans != 1.0f;
   if (P.persistent && whitted && env_int("DRT_WHITTED_TWO_PASS", 1) != 0 && aa2 != 0 &&
       (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
-      (F.mode == MODE_WHITTED_QUAD ? F.grid_res >= 4 || aa2 >= 2 : big_frame) &&
+      (F.mode == MODE_WHITTED_QUAD ? F.grid_res >= 4 || aa2 >= 2 : big_frame || grid_mixed) &&
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) && !(p->flags & DRT_FRAME_REFERENCE_ORDER) &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
     P.two_pass = P.aa_chain = true;
