@@ -1035,7 +1035,15 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // The Grid's AA frames too (its shadow queries stay on the Grid: Grid::Traverse(Ray&)'s answer is
   // tied to the cells its walk visits): 1 381 against 1 295 Mrays/s on the Grid headline scene.
   const bool grid_chain = c->accel == DRT_ACCEL_GRID && c->has_grid && env_int("DRT_AA_TWO_PASS_GRID", 1) != 0;
-  if (P.persistent && F.mode == MODE_AA && big_frame && (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
+  // Scenes of mixed primitives without a refracting material take two passes at any size (round 5): their
+  // one-pass kernel is the mixed-primitive path kernel (BVH 67, Grid 79 VGPR spills), while the chain pass
+  // and the wavefront's shadow stream run at 7 waves/SIMD — the shipped balls_high (7 383 spheres) AA16
+  // frame: BVH 5 275 -> 6 287, Grid 2 254 -> 2 415 Mrays/s; its Whitted frame on the Grid 3.48 -> 2.05
+  // ms.  Triangle scenes' small frames and glass scenes' tree frames measured slower in two passes
+  // (dragon AA16: BVH 5 887 -> 3 277; profiles/r05_whitted_two_pass_wavefront.jsonl, r05_gvb_aa_two_pass.jsonl).
+  bool mixed_noglass = !c->tri_only;
+  for (const drt_material& m : c->mats) mixed_noglass = mixed_noglass && m.trans != 1.0f;
+  if (P.persistent && F.mode == MODE_AA && (big_frame || mixed_noglass) && (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
       c->n_prims >= env_int("DRT_AA_TWO_PASS_MIN_PRIMS", 1024) &&
       !(p->flags & DRT_FRAME_REFERENCE_ORDER) && aa2 != 0 &&
       P.n_slots < kPersistentMaxItems && P.n_slots * (uint64_t)(md + 1) * 8u <= kTwoPassMaxBytes) {
@@ -1048,16 +1056,11 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   // (BVH) or the Grid.  Same conditions as the AA frames'; a quad-light frame of >= 4 light samples
   // at any size (the closest work shrinks grid_res times), a point-light frame by the AA size rule.
   // DRT_WHITTED_TWO_PASS=0 keeps one pass.
-  // A Grid scene of mixed primitives without a refracting material takes two passes at any size: its
-  // one-pass kernel is the mixed-primitive Grid stepper at 5 waves/SIMD (79 VGPR spills), while the
-  // chain pass and the wavefront's shadow stream run at 7 — the shipped balls_high Whitted frame (7 383
-  // spheres, point light) 3.48 -> 2.05 ms at 512^2 and 4.87 -> 3.76 ms at 1024^2, where the triangle
-  // scenes' point-light frames (dragon) and the glass scene's tree frames (assignment1) measured 8-50 %
-  // slower in two passes (profiles/r05_whitted_two_pass_wavefront.jsonl).
+  // (A Grid scene of mixed primitives without a refracting material: point-light Whitted frames in two
+  // passes at any size too, mixed_noglass above; measured on the Grid only.)
   P.chain_div = 1;
   const bool whitted = F.mode == MODE_WHITTED_QUAD || F.mode == MODE_WHITTED_POINT;
-  bool grid_mixed = grid_chain && !c->tri_only;
-  for (const drt_material& m : c->mats) grid_mixed = grid_mixed && m.trans != 1.0f;
+  const bool grid_mixed = grid_chain && mixed_noglass;
   if (P.persistent && whitted && env_int("DRT_WHITTED_TWO_PASS", 1) != 0 && aa2 != 0 &&
       (grid_chain || (c->accel == DRT_ACCEL_BVH && c->has_bvh && c->has_wide)) &&
       (F.mode == MODE_WHITTED_QUAD ? F.grid_res >= 4 || aa2 >= 2 : big_frame || grid_mixed) &&
