@@ -26,6 +26,8 @@ void launch_trace_stream(const SceneArgs& S, const TraceArgs& A, bool shadow, bo
 void launch_trace_prep(const float* rays, int n, int shadow, float4* out, hipStream_t st);
 void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
 void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
+void launch_wf_combine_reduce(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, const ReduceArgs& R,
+                              hipStream_t st);
 void launch_trace_finish(const SceneArgs& S, const float4* q, int n, float* t, const uint32_t* prim, float* nrm,
                          int32_t* obj, hipStream_t st);
 void launch_trace(const SceneArgs& S, int accel, bool tri_only, const float* rays, int n, int shadow, float* t,
@@ -46,6 +48,14 @@ struct DevBuf {
     bytes = 0;
   }
   hipError_t ensure(size_t n) {  // grow-only
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc(&p, n ? n : 16);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  hipError_t fit(size_t n) {  // grow, and give back a buffer far larger than this use needs
+    if (p && bytes > 4 * n + (256u << 20)) release();
     if (n <= bytes && p) return hipSuccess;
     release();
     hipError_t e = hipMalloc(&p, n ? n : 16);
@@ -90,7 +100,7 @@ struct drt_ctx {
   // 4-ary shadow tree collapsed from the BVH (drt_layout.hpp); absent for a leaf root, a tree too
   // deep for the shadow stack, coordinates no record can quantise, or DRT_WIDE_SHADOW=0
   bool has_wide = false;
-  DevBuf d_wnodes, d_wleaf;
+  DevBuf d_wnodes, d_wleaf;  // the shadow tree's 48-B records (nodes + leaf copies), leaf box per record
   uint32_t wroot = 0, n_wide = 0;
   // grid
   bool has_grid = false;
@@ -285,13 +295,19 @@ static bool wide_tree_valid(const drt_bvh_node* nodes, uint32_t n_nodes, uint32_
   return leaf_objs == n_obj;
 }
 
-// Collapse the reference's binary tree (nodes, leaf descriptors per node) into 4-ary records: a
-// wide node's children are its binary node's two children, the inner one with the largest box
-// surface replaced by its two children until there are four (or only leaves).  Records in depth-
-// first order.  False if a record cannot be quantised or 3 * depth would overflow the shadow stack.
-static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& leaf_descs,
-                       std::vector<WideNodeRecord>& out, uint32_t& root) {
+// Collapse the reference's binary tree into 4-ary records (drt_layout.hpp): a wide node's children are its
+// binary node's two children, the inner one with the largest box surface replaced by its two children
+// until there are four (or only leaves).  One array of 48-B records: the root's node record first, then
+// per wide node (depth-first) its block — its inner children's node records, then its leaf children's
+// primitives (copies of `prims`, the records in BVH object order; q2.w = 1 while the leaf continues),
+// leaves by ascending count so that the block's offsets stay small — and per record index the exact
+// reference leaf box of a copied primitive (`lbox`).  False if a record cannot be quantised, a block
+// offset passes kWideMaxOffset (two oversized leaves under one wide node) or 3 * depth would overflow
+// the shadow stack; the scene then keeps the binary tree for its shadow queries.
+static bool build_wide(const drt_bvh_node* nodes, const std::vector<PrimRecord>& prims, std::vector<PrimRecord>& out,
+                       std::vector<LeafBoxRecord>& lbox, uint32_t& root) {
   out.clear();
+  lbox.clear();
   if (nodes[0].leaf) return false;
   auto area = [&](uint32_t i) {
     const drt_bvh_node& nd = nodes[i];
@@ -305,7 +321,10 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
   };
   std::vector<Item> st{{0u, 0u, 1}};
   const int order = env_int("DRT_WIDE_ORDER", 2);
+  out.reserve(prims.size() + prims.size() / 2 + 1);
   out.emplace_back();
+  lbox.reserve(out.capacity() + 2);
+  lbox.emplace_back();  // a node record's entry stays zero
   int maxd = 1;
   while (!st.empty()) {
     const Item it = st.back();
@@ -328,6 +347,11 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
       ch[best] = nodes[c].index;
       ch[n++] = nodes[c].index + 1;
     }
+    // a leaf without objects can never report a hit: its slot stays unused (an inverted box)
+    int m = 0;
+    for (int k = 0; k < n; k++)
+      if (!nodes[ch[k]].leaf || nodes[ch[k]].n_objs > 0) ch[m++] = ch[k];
+    n = m;
     // child slot order: the device enters the first hit slot, then the others in slot order.  Default
     // 2, ascending box surface (0: as collapsed, 1: descending, 3: leaves first, then descending)
     if (order == 1 || order == 2 || order == 3) {
@@ -339,27 +363,55 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
     WideNodeRecord r{};
     for (int a = 0; a < 3; a++) {
       double lo[4], hi[4];
+      lo[0] = hi[0] = 0.0;
       for (int k = 0; k < n; k++) {
         lo[k] = nodes[ch[k]].bmin[a];
         hi[k] = nodes[ch[k]].bmax[a];
       }
       uint32_t e = 0;
-      if (!quantize_axis(lo, hi, n, r.p[a], e, r.q[2 * a], r.q[2 * a + 1])) return false;
+      if (!quantize_axis(lo, hi, std::max(n, 1), r.p[a], e, r.q[2 * a], r.q[2 * a + 1])) return false;
       r.ebits |= e << (8 * a);
     }
-    // children pushed in reverse so the first child's subtree follows its parent in memory
-    for (int k = n - 1; k >= 0; k--) {
-      if (nodes[ch[k]].leaf) {
-        r.desc[k] = leaf_descs[ch[k]];
-      } else {
-        r.desc[k] = (uint32_t)out.size();
-        out.emplace_back();
-        st.push_back({ch[k], r.desc[k], it.depth + 1});
-      }
+    if (n == 0) {  // (every child an empty leaf) no slot is hit
+      for (int a = 0; a < 3; a++) r.q[2 * a] = 0xffffffffu, r.q[2 * a + 1] = 0u;
     }
-    out[it.slot] = r;
+    // the block: inner children in slot order, then the leaves' primitives by ascending count
+    const uint32_t base = (uint32_t)out.size();
+    r.base = base;
+    int inner[4], leaves[4], ni = 0, nl = 0;
+    for (int k = 0; k < n; k++) (nodes[ch[k]].leaf ? leaves[nl++] : inner[ni++]) = k;
+    std::stable_sort(leaves, leaves + nl, [&](int a, int b) { return nodes[ch[a]].n_objs < nodes[ch[b]].n_objs; });
+    uint32_t off = 0;
+    for (int j = 0; j < ni; j++) {
+      r.offs |= off << (8 * inner[j]);
+      out.emplace_back();
+      lbox.emplace_back();
+      off++;
+    }
+    for (int j = 0; j < nl; j++) {
+      const int k = leaves[j];
+      if (off > kWideMaxOffset) return false;
+      const drt_bvh_node& nd = nodes[ch[k]];
+      r.offs |= off << (8 * k);
+      r.ebits |= 1u << (24 + k);
+      LeafBoxRecord b{};
+      memcpy(b.box, nd.bmin, 12);
+      memcpy(b.box + 3, nd.bmax, 12);
+      for (uint32_t i = 0; i < nd.n_objs; i++) {
+        PrimRecord pr = prims[nd.index + i];
+        pr.q[11] = bits_as_float(i + 1 < nd.n_objs ? 1u : 0u);
+        out.push_back(pr);
+        lbox.push_back(b);
+      }
+      off += nd.n_objs;
+    }
+    if ((uint64_t)out.size() >= 0x7fffffffull) return false;
+    memcpy(&out[it.slot], &r, sizeof(r));
+    // children pushed in reverse, so that the first inner child's block follows this one
+    for (int j = ni - 1; j >= 0; j--) st.push_back({ch[inner[j]], base + (uint32_t)j, it.depth + 1});
   }
   if (3 * maxd > kWideMaxStack) return false;
+  lbox.resize(out.size() + 2);  // (+ 2: zeroed tail records for the node step's slot reads)
   root = 0;
   return true;
 }
@@ -629,23 +681,16 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
     r.desc[1] = dsc[nodes[i].index + 1];
     r.desc[2] = r.desc[3] = 0;
   }
-  // 4-ary shadow tree and the exact reference leaf box of every primitive (DRT_WIDE_SHADOW=0: none)
-  std::vector<WideNodeRecord> wide;
+  // primitive records in BVH object order: every leaf is one contiguous run
+  std::vector<PrimRecord> perm(n_obj);
+  for (uint32_t i = 0; i < n_obj; i++) perm[i] = c->prims_scene[order[i]];
+  // 4-ary shadow tree: wide nodes and leaf-primitive copies in one 48-B record array, and the exact
+  // reference leaf box per record (DRT_WIDE_SHADOW=0: none)
+  std::vector<PrimRecord> wide;
+  std::vector<LeafBoxRecord> lbox;
   uint32_t wroot = 0;
   const bool has_wide = env_int("DRT_WIDE_SHADOW", 1) != 0 && wide_tree_valid(nodes, n_nodes, n_obj) &&
-                        build_wide(nodes, dsc, wide, wroot);
-  std::vector<LeafBoxRecord> lbox;
-  if (has_wide) {
-    lbox.assign((size_t)n_obj + 2, LeafBoxRecord{});  // + 2: the node step's tail slot reads
-    for (uint32_t i = 0; i < n_nodes; i++) {
-      const drt_bvh_node& nd = nodes[i];
-      if (!nd.leaf) continue;
-      LeafBoxRecord b{};
-      memcpy(b.box, nd.bmin, 12);
-      memcpy(b.box + 3, nd.bmax, 12);
-      for (uint32_t k = 0; k < nd.n_objs; k++) lbox[nd.index + k] = b;
-    }
-  }
+                        build_wide(nodes, perm, wide, lbox, wroot);
   // depth (= bound on the traversal stack), iterative
   int maxd = 0;
   {
@@ -670,8 +715,9 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
   if (!recs.empty()) DRT_HIP(c, hipMemcpy(c->d_nodes.p, recs.data(), sizeof(NodeRecord) * recs.size(), hipMemcpyHostToDevice));
   c->has_wide = false;
   if (has_wide) {
-    DRT_HIP(c, c->d_wnodes.ensure(sizeof(WideNodeRecord) * wide.size()));
-    DRT_HIP(c, hipMemcpy(c->d_wnodes.p, wide.data(), sizeof(WideNodeRecord) * wide.size(), hipMemcpyHostToDevice));
+    wide.resize(wide.size() + 2);  // zeroed tail records (slot reads past a block's last record)
+    DRT_HIP(c, c->d_wnodes.ensure(sizeof(PrimRecord) * wide.size()));
+    DRT_HIP(c, hipMemcpy(c->d_wnodes.p, wide.data(), sizeof(PrimRecord) * wide.size(), hipMemcpyHostToDevice));
     DRT_HIP(c, c->d_wleaf.ensure(sizeof(LeafBoxRecord) * lbox.size()));
     DRT_HIP(c, hipMemcpy(c->d_wleaf.p, lbox.data(), sizeof(LeafBoxRecord) * lbox.size(), hipMemcpyHostToDevice));
     c->wroot = wroot;
@@ -680,9 +726,6 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
   }
   DRT_HIP(c, c->d_big.ensure(sizeof(uint2) * std::max<size_t>(1, big.size())));
   if (!big.empty()) DRT_HIP(c, hipMemcpy(c->d_big.p, big.data(), sizeof(uint2) * big.size(), hipMemcpyHostToDevice));
-  // primitive records in BVH object order: every leaf is one contiguous run
-  std::vector<PrimRecord> perm(n_obj);
-  for (uint32_t i = 0; i < n_obj; i++) perm[i] = c->prims_scene[order[i]];
   DRT_HIP(c, hipMemcpy(c->d_prims.p, perm.data(), sizeof(PrimRecord) * perm.size(), hipMemcpyHostToDevice));
   c->has_bvh = true;
   c->has_grid = false;
@@ -726,8 +769,8 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   // 132 instead of 158 MB at 1M triangles.  A cell's list starts on a pair boundary: cell_tpos[i] is
   // its first record (even), bit 31 set when cell i - 1's list ended on a padding slot, so a cell's
   // range is [tpos[i], tpos[i + 1] - pad) from one 8-B load.
-#ifdef DRT_GRID_RECS48
-  const bool packed = false;  // (A/B) the 48-B records for every scene
+#if defined(DRT_GRID_RECS48) || defined(DRT_GRID_INDEXED)
+  const bool packed = false;  // (A/B) the 48-B records for every scene (the indexed layout's too)
 #else
   const bool packed = c->tri_only;
 #endif
@@ -917,6 +960,7 @@ struct Plan {
   bool wavefront;       // two-pass frame without refraction: pass 2 as wf_gen + shadow-query stream + wf_combine
   uint64_t wf_chunk;    // ... over chunks of this many sample slots
   uint32_t wf_chunks;
+  bool wf_fold;         // ... with the reduce folded into wf_combine (no reduce launch, no sample buffer)
   bool skip;            // progressive frame past MAX_SAMPLES: nothing to render
   uint64_t n_slots;     // float4 sample slots of the frame (reduce reads nsub per pixel)
 };
@@ -1106,16 +1150,30 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
   P.wavefront = false;
   P.wf_chunk = 0;
   P.wf_chunks = 0;
+  P.wf_fold = false;
   if (P.two_pass && !P.tree && (c->accel == DRT_ACCEL_BVH || c->accel == DRT_ACCEL_GRID) &&
       env_int("DRT_WAVEFRONT", 1) != 0 && (c->accel == DRT_ACCEL_BVH || env_int("DRT_WAVEFRONT_GRID", 1) != 0) &&
       (P.aa_chain || env_int("DRT_WAVEFRONT_INORDER", 1) != 0)) {
-    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(P.n_slots, env_u64("DRT_WAVEFRONT_CHUNK_SLOTS", 1ull << 24)));
-    const uint64_t q = ((uint64_t)md + 1u) * wf_pairs(c, F.light_spp) * (chunk + 8u);
+    // the chunk: at most DRT_WAVEFRONT_CHUNK_SLOTS slots and DRT_WAVEFRONT_CHUNK_BYTES of query buffers
+    // (round 6, ADVICE r5: many lights x light_spp made a fixed 2^24-slot chunk ask for ~160 GB), whole
+    // pixels (a multiple of nsub, so that wf_combine can fold the reduce)
+    const uint64_t pairs = wf_pairs(c, F.light_spp);
+    const uint64_t slot_bytes = ((uint64_t)md + 1u) * (pairs * 41u + 16u);
+    const uint64_t budget = env_u64("DRT_WAVEFRONT_CHUNK_BYTES", 24ull << 30);
+    uint64_t chunk = std::min<uint64_t>(P.n_slots, env_u64("DRT_WAVEFRONT_CHUNK_SLOTS", 1ull << 24));
+    chunk = std::min<uint64_t>(chunk, budget / std::max<uint64_t>(1, slot_bytes));
+    const uint64_t px = (uint64_t)std::max(1, slots);
+    if (chunk > px) chunk -= chunk % px;
+    chunk = std::max<uint64_t>(1, chunk);
+    const uint64_t q = ((uint64_t)md + 1u) * pairs * (chunk + 8u);
     const uint64_t chunks = (P.n_slots + chunk - 1) / chunk;
-    if (P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems && chunks <= 64) {
+    if (P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems && chunks <= 4096) {
       P.wavefront = true;
       P.wf_chunk = chunk;
       P.wf_chunks = (uint32_t)chunks;
+      // the reduce folded into wf_combine (whole pixels per chunk, <= 1024 samples per pixel; a wavefront
+      // frame is never progressive); DRT_WAVEFRONT_FOLD=0 keeps the separate reduce launch
+      P.wf_fold = chunk % px == 0 && px <= 1024 && prog == 0 && env_int("DRT_WAVEFRONT_FOLD", 1) != 0;
     }
   }
   ReduceArgs& R = P.R;
@@ -1268,6 +1326,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       P.F.seq_backlog = (uint32_t)std::max(0, env_int("DRT_SEQ_BACKLOG", 0));
     }  // with pairs 3, 5 waves: 1 300 Mrays/s; (walk, pairs) = (8, 4) 1 228, (6, 3) 1 272, (4, 3) 1 235-1 319, (5, 2) 1 275
   }
+  bool folded = false;  // the reduce ran inside wf_combine
   if (P.F.n_items && P.two_pass) {
     DevBuf& d_rk = c->d_skel_rk_s[slot];  // allocated above
     DevBuf& d_hits = c->d_skel_hits_s[slot];
@@ -1277,10 +1336,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     if (P.wavefront) {
       const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
       const uint64_t q = levels * pairs * (P.wf_chunk + 8u);  // (+ the last band's padding, wf_q)
-      if (c->d_wf_rays_s[slot].ensure(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_nl_s[slot].ensure(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_occ_s[slot].ensure(std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_lvl_s[slot].ensure(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
+      if (c->d_wf_rays_s[slot].fit(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_nl_s[slot].fit(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_occ_s[slot].fit(std::max<uint64_t>(q, 1)) == hipSuccess &&
+          c->d_wf_lvl_s[slot].fit(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
         wavefront = true;
         W.rays = c->d_wf_rays_s[slot].as<float4>();
         W.rays_b = W.rays + std::max<uint64_t>(q, 1);
@@ -1397,9 +1456,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);
         DRT_HIP(c, hipGetLastError());
       }
-      launch_wf_combine(S, F2, W, st);
+      if (P.wf_fold) launch_wf_combine_reduce(S, F2, W, P.R, st);
+      else launch_wf_combine(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
     }
+    folded = wavefront && P.wf_fold;
     if (!wavefront) launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
   } else if (P.F.n_items) {
     if (persistent) launch_path_persistent(S, P.F, c->accel, c->tri_only, stats, st);
@@ -1410,7 +1471,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   DRT_HIP(c, hipEventRecord(ev[1], st));
   DRT_HIP(c, hipEventRecord(c->ev_path[slot], st));  // every frame: the slot's last path kernel
   c->path_issued[slot] = true;
-  if (P.F.n_my_tiles) {
+  if (P.F.n_my_tiles && !folded) {
     if (use_aux) DRT_HIP(c, hipStreamWaitEvent(ax, c->ev_path[slot], 0));
     launch_reduce(P.R, ax);
     DRT_HIP(c, hipGetLastError());

@@ -978,7 +978,7 @@ __device__ __forceinline__ DdaState dda_step(DdaState d, const DdaAxes& a, bool 
 // records for every scene (A/B)
 template <bool TRI_ONLY>
 constexpr bool kGridPacked =
-#ifdef DRT_GRID_RECS48
+#if defined(DRT_GRID_RECS48) || defined(DRT_GRID_INDEXED)  // (the indexed A/B layout uses the 48-B records)
     false;
 #else
     TRI_ONLY;
@@ -1218,18 +1218,21 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   const bool verify = WIDE && visit && (fl & LF_VERIFY) != 0u;
   const bool inner = visit && !verify && !desc_is_leaf(cur);
   const bool leaf = visit && !verify && desc_is_leaf(cur);
-  uint32_t first = desc_first(cur), cnt = desc_count(cur);
-  const bool big = leaf && cnt == kBigLeaf;
+  // a shadow-tree lane's leaf is the record of its next primitive in the shadow tree's array, tested one
+  // per step whatever LEAF1 is (the record's q2.w says whether the leaf goes on; drt_layout.hpp)
+  uint32_t first = wide ? (cur & ~kLeafBit) : desc_first(cur), cnt = wide ? 1u : desc_count(cur);
+  const bool big = leaf && !wide && cnt == kBigLeaf;
   // LEAF1 1 / 2: one primitive of a leaf per step (below), 2 also leaving the last slot unread for
   // such a step; 0: the whole leaf in the step
-  const bool whole = LEAF1 == 0 || big;
+  const bool whole = !wide && (LEAF1 == 0 || big);
   if (big) {  // oversized leaf: (first, count) from the side table
     const uint2 bl = S.big_leaves[first];
     first = bl.x;
     cnt = bl.y;
   }
-  const float4* rec = leaf ? S.prims + 3 * (size_t)first
-                           : (verify ? S.wleaf + 2 * (size_t)cur : (wide ? S.wnodes : S.nodes) + 4 * (size_t)cur);
+  // (a shadow-tree record is 48 B, node or primitive copy; a leaf-box check reads 32 B)
+  const float4* rec = verify ? S.wleaf + 2 * (size_t)cur
+                             : (wide ? S.wnodes + 3 * (size_t)first : (leaf ? S.prims + 3 * (size_t)first : S.nodes + 4 * (size_t)cur));
   float4 s0, s1, s2, s3, s4, s5;
   bool uni_done = false;
   if (UNI && visit) {
@@ -1252,13 +1255,15 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   if (visit && !uni_done) {
     s0 = rec[0];
     s1 = rec[1];
-    s2 = rec[2];
+    if (!(WIDE && verify)) s2 = rec[2];  // (a leaf box is two slots)
     // (Measured alternative, kept out: an 8-B load of the last slot for inner nodes, which use
     // only its two child descriptors: the split into two masked loads cost 8.6 %.)
     // The last slot serves inner nodes (child descriptors) and whole-leaf steps (the second
     // primitive's first slot); a one-primitive leaf step does not read it (LEAF1 2: +1.3 % on the
     // headline; the closest-chain pass of in-order frames lost 1.5 % with it and keeps 1).
-    if (LEAF1 != 2 || inner || whole) s3 = rec[3];
+    // A shadow-tree lane never reads a fourth slot (round 6: its records are 48 B, so a shadow step issues
+    // three loads where the 64-B records of rounds 4-5 took four).
+    if ((LEAF1 != 2 || inner || whole) && !wide) s3 = rec[3];
   }
   if (leaf && whole && cnt > 1) {
     s4 = rec[4];
@@ -1285,7 +1290,11 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     const bool px = L.q.sx(), py = L.q.sy(), pz = L.q.sz();
     const uint32_t nx = px ? lx : hx, fx = px ? hx : lx, ny = py ? ly : hy, fy = py ? hy : ly, nz = pz ? lz : hz,
                    fz = pz ? hz : lz;
-    const uint32_t d[4] = {__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w)};
+    // child k: record base + byte k of offs, a leaf (its first primitive's record) if bit 24 + k of s0.w is set
+    const uint32_t base = __float_as_uint(s2.z), offs = __float_as_uint(s2.w);
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = (base + ((offs >> (8 * k)) & 0xffu)) | (((eb >> (24 + k)) & 1u) << 31);
     float tn[4];
     bool hk[4];
 #ifdef DRT_WIDE_PK
@@ -1494,8 +1503,8 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     // four loads fetch it with the other lanes' nodes: the rest of the leaf is itself a leaf
     // descriptor.  (The second primitive's two slots loaded beside the first, for the few lanes
     // with such a leaf, cost a load instruction each at a per-instruction floor: tools/td_lanes.hip.)
-    const bool more = !whole && !done && cnt > 1;
-    if (more) L.cur = leaf_desc(first + 1, cnt - 1);
+    const bool more = wide ? !done && __float_as_uint(s2.w) != 0u : !whole && !done && cnt > 1;
+    if (more) L.cur = wide ? (kLeafBit | (first + 1u)) : leaf_desc(first + 1, cnt - 1);
     fl = more ? (fl | LF_LEAFCONT) : (fl & ~LF_LEAFCONT);
     if (!more && (fl & LF_TRAV) && !(WIDE && (fl & LF_VERIFY))) fl |= LF_POP;
   }
@@ -2510,7 +2519,9 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
           // (interleaved records: rays_b = rays + 1, stride 2; or two arrays, stride 1)
           const size_t at = (size_t)it * (uint32_t)A.stride;
           const float4 a = A.rays[at];
-          if (!A.sparse || a.w >= 0.0f) {
+          // (an empty slot is thr < 0, wf_mark_empty; a NaN range is a query, answered 0, as MODE_QSTREAM
+          // answers it — ADVICE r5: skipping it left a stale answer in occ_out)
+          if (!A.sparse || !(a.w < 0.0f)) {
           const float4 b = A.rays_b[at];
           L.item = it;
           L.q = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
@@ -2634,17 +2645,11 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
   wf_mark_empty(W, l, slot);
 }
 
-__global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
-  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= W.n_slots) return;
-  const uint32_t g = W.slot0 + slot;
+// One sample's colour from its level records and shadow answers: the levels walked back from the last
+// one, the unshadowed light terms added in the light loop's pair order, the depth cut and the mirror unwind.
+__device__ __forceinline__ V3 wf_sample(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, uint32_t slot) {
   const size_t ns = W.n_slots;
-  const int md = F.max_depth, np = W.pairs;
-  const Item it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
-  if (!it.valid) {  // padding of a partial tile
-    F.samples[g] = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
+  const int md = F.max_depth;
   // the last level of the chain: a miss, the depth cut, or a hit without a mirror child
   int last = 0;
   for (; last < md; last++) {
@@ -2678,7 +2683,66 @@ __global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs 
       c = cclamp(acc);
     }
   }
+  return c;
+}
+
+__global__ void __launch_bounds__(256) wf_combine_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= W.n_slots) return;
+  const uint32_t g = W.slot0 + slot;
+  const Item it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
+  const V3 c = it.valid ? wf_sample(S, F, W, slot) : mk(0, 0, 0);  // (zero: padding of a partial tile)
   F.samples[g] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+// The pixel's framebuffer value, as reduce_kernel writes it: the ordered sum over its nsub sample colours
+// (Color +=, main.cpp:664 / :694), times the scale (main.cpp:666 / :696), to the frame or the shard buffer.
+__device__ __forceinline__ float* reduce_target(const ReduceArgs& A, uint32_t pidx) {
+  if (A.full_frame) {
+    const uint32_t per_tile = (uint32_t)(A.tile * A.tile);
+    const uint32_t k = pidx / per_tile, pix = pidx - k * per_tile;
+    uint32_t tx, ty;
+    tile_of_position(A.shard + k * A.n_shards, A.tiles_x, tx, ty);
+    const int x = (int)(tx * A.tile + pix % A.tile);
+    const int y = (int)(ty * A.tile + pix / A.tile);
+    if (x >= A.res_x || y >= A.res_y) return nullptr;
+    return A.out + 3 * ((size_t)y * A.res_x + x);
+  }
+  return A.out + 3 * (size_t)pidx;
+}
+
+// wf_combine with the frame's reduce folded in (round 6): a block holds `ppb` whole pixels (ppb x nsub
+// sample slots, nsub <= 1024), every thread combines its sample into LDS, then one thread per (pixel,
+// channel) adds the pixel's samples in sample order — the same float additions, in the same order, as
+// reduce_kernel — and writes the scaled value.  No sample buffer is written or read back, and a wavefront
+// frame is one launch shorter.
+__global__ void __launch_bounds__(1024) wf_combine_reduce_kernel(SceneArgs S, FrameArgs F, WfArgs W, ReduceArgs R,
+                                                                 uint32_t ppb) {
+  __shared__ float sc[3][1024];
+  const uint32_t nsub = (uint32_t)R.nsub, per_block = ppb * nsub, t = threadIdx.x;
+  const uint32_t base = blockIdx.x * per_block;  // the block's first chunk slot (a pixel's first sample)
+  if (t < per_block) {
+    const uint32_t slot = base + t;
+    V3 c = mk(0, 0, 0);
+    if (slot < W.n_slots) {
+      const Item it = decode_item(F, S.res_x, S.res_y, W.slot0 + slot, F.nsub);
+      if (it.valid) c = wf_sample(S, F, W, slot);
+    }
+    sc[0][t] = c.x;
+    sc[1][t] = c.y;
+    sc[2][t] = c.z;
+  }
+  __syncthreads();
+  for (uint32_t w = t; w < 3u * ppb; w += blockDim.x) {  // (nsub < 3: more (pixel, channel) pairs than threads)
+    const uint32_t p = w / 3u, ch = w - 3u * p;
+    if (base + p * nsub >= W.n_slots) break;
+    const float* v = sc[ch] + p * nsub;
+    float r = 0.f;
+#pragma unroll 8
+    for (uint32_t i = 0; i < nsub; i++) r += v[i];
+    float* o = reduce_target(R, (W.slot0 + base) / nsub + p);
+    if (o) o[ch] = r * R.scale;
+  }
 }
 
 void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {
@@ -2687,6 +2751,14 @@ void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipS
 }
 void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st) {
   hipLaunchKernelGGL(wf_combine_kernel, dim3((W.n_slots + 255) / 256), dim3(256), 0, st, S, F, W);
+}
+// (the caller checks wf_can_fold_reduce: whole pixels per chunk, nsub <= 1024, not progressive)
+void launch_wf_combine_reduce(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, const ReduceArgs& R,
+                              hipStream_t st) {
+  const uint32_t nsub = (uint32_t)R.nsub, ppb = nsub >= 256u ? 1u : 256u / nsub, per_block = ppb * nsub;
+  const uint32_t threads = (per_block + 63u) & ~63u;
+  hipLaunchKernelGGL(wf_combine_reduce_kernel, dim3((W.n_slots + per_block - 1) / per_block), dim3(threads), 0, st, S,
+                     F, W, R, ppb);
 }
 
 // Batched-query front end: rays n x {ox,oy,oz,dx,dy,dz} -> streaming-query records with the
@@ -2728,26 +2800,15 @@ __global__ void __launch_bounds__(256) trace_finish_kernel(SceneArgs S, const fl
 // Ordered sum over a pixel's items (Color += in sample order, main.cpp:664 / :694) and scale.
 __global__ void __launch_bounds__(256) reduce_kernel(ReduceArgs A) {
   const uint32_t pidx = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t per_tile = (uint32_t)(A.tile * A.tile);
-  if (pidx >= (uint32_t)A.n_my_tiles * per_tile) return;
+  if (pidx >= (uint32_t)A.n_my_tiles * (uint32_t)(A.tile * A.tile)) return;
   float r = 0.f, g = 0.f, b = 0.f;
   const float4* s = A.samples + (size_t)pidx * A.nsub;
   for (int i = 0; i < A.nsub; i++) {
     float4 v = s[i];
     r += v.x; g += v.y; b += v.z;
   }
-  float* o;
-  if (A.full_frame) {
-    const uint32_t k = pidx / per_tile, pix = pidx - k * per_tile;
-    uint32_t tx, ty;
-    tile_of_position(A.shard + k * A.n_shards, A.tiles_x, tx, ty);
-    const int x = (int)(tx * A.tile + pix % A.tile);
-    const int y = (int)(ty * A.tile + pix / A.tile);
-    if (x >= A.res_x || y >= A.res_y) return;
-    o = A.out + 3 * ((size_t)y * A.res_x + x);
-  } else {
-    o = A.out + 3 * (size_t)pidx;
-  }
+  float* o = reduce_target(A, pidx);
+  if (!o) return;
   if (A.prog_frame > 1) {  // lerp(a, b, t) = a + t * (b - a) in double (maths.h:56), t = 1.0 / FrameCount
     const double t = 1.0 / (double)A.prog_frame;
     o[0] = (float)((double)o[0] + t * ((double)r - (double)o[0]));

@@ -211,24 +211,33 @@ typedef struct {
   int32_t persistent;
   int32_t tiles_in_shard;
   int32_t passes;      /* 2: a pass over the samples' closest hits and a pass over every sample with
-                          its closest hits read back; 1 otherwise.  Two passes for: in-order frames
-                          (DoF / glossy) of scenes without refraction (a pixel's samples in order);
-                          AA frames of BVH / Grid scenes of >= 1024 objects whose whole frame has
-                          >= 2^23 samples or whose scene has >= 2^19 objects; Whitted frames of such
-                          scenes (quad light 0: at any size, one closest-hit chain per pixel shared
-                          by its gridRes light samples; point light: the AA size rule).  With a
-                          refracting material the AA / Whitted passes record each sample's whole
-                          closest-hit tree (<= 2^(max_depth+1) - 1 hits) if it fits 32 GB.  The
+                          its closest hits read back; 1 otherwise.  Two passes for:
+                          - in-order frames (DoF / glossy) of scenes without refraction (a pixel's
+                            samples in order);
+                          - AA frames of BVH (shadow tree uploaded) / Grid scenes of >= 1024 objects
+                            whose whole frame has >= 2^23 samples or whose scene has >= 2^19 objects,
+                            and at any size when the scene has non-triangle primitives and no
+                            refracting material;
+                          - Whitted frames of such scenes: quad light 0 at any size (one closest-hit
+                            chain per pixel shared by its gridRes light samples); point light by the
+                            AA size rule, and at any size on a Grid scene of mixed primitives without
+                            a refracting material.
+                          With a refracting material the AA / Whitted passes record each sample's
+                          whole closest-hit tree (<= 2^(max_depth+1) - 1 hits) if it fits 32 GB.  The
                           plan depends on the params and the uploaded scene only, and drt_render
                           follows it.  Both plans render the same frame; the stats differ only in
                           where shadow work is counted (shadow_* on the reference tree, wide_* on
                           the shadow tree) and, for quad-light Whitted frames, in closest_* (gridRes
                           times fewer traversals). */
   int32_t wavefront;   /* 1: pass 2 of this two-pass frame runs as a wavefront — every shadow query of
-                          the frame generated from the recorded closest hits, answered by the
-                          streaming traversal kernel, combined per sample (AA / Whitted frames of
-                          BVH scenes without refraction, < 2^32 query slots; DRT_WAVEFRONT=0: the
-                          persistent replay).  A frame whose query buffers cannot be allocated runs
+                          the frame generated from the recorded closest hits, answered by a streaming
+                          kernel (BVH: trace_stream on the shadow tree; Grid: its stepper's query
+                          stream), then combined per sample with the frame's reduce folded in.  Every
+                          two-pass frame without refraction: AA, Whitted and in-order (DoF / glossy)
+                          frames, BVH and Grid (< 2^32 query slots; the query buffers in chunks of at
+                          most DRT_WAVEFRONT_CHUNK_BYTES, default 24 GB, per frame slot).
+                          DRT_WAVEFRONT=0 (DRT_WAVEFRONT_GRID=0, DRT_WAVEFRONT_INORDER=0 per kind):
+                          the persistent replay.  A frame whose query buffers cannot be allocated runs
                           the persistent replay, which renders the same frame. */
   int32_t reserved[3];
 } drt_frame_plan;

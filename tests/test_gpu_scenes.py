@@ -34,12 +34,17 @@ SCENE_CASES = {
     "dragon_grid_whitted_sky": ("dragon", {}, {}),
     "assignment1_grid_whitted_sky": ("assignment1", {}, {}),
     "dragon_assignment1_bvh_whitted_sky": ("dragon_assignment1", {}, {}),
-    "dragon_assignment1_bvh_aa16": ("dragon_assignment1", dict(res=(256, 256), spp=16), {}),
     # round 5: AA frames of scenes with glass (trans 1) run as MODE_TCHAIN + MODE_TREPLAY two-pass frames
-    # in this suite (DRT_AA_TWO_PASS=2, tests/conftest.py)
-    "balls_high_bvh_aa16_glass": ("balls_high", dict(accel="bvh", res=(192, 192), spp=16), {}),
+    # in this suite (DRT_AA_TWO_PASS=2, tests/conftest.py): dragon_assignment1 on the BVH (the tree replay's
+    # shadow queries on the shadow tree), assignment1 on the Grid (TREE_CASES below checks the plan);
+    # blueDiamond's 178 objects keep the one-pass glass frame (DRT_AA_TWO_PASS_MIN_PRIMS)
+    "dragon_assignment1_bvh_aa16_glass": ("dragon_assignment1", dict(res=(256, 256), spp=16), {}),
+    "blueDiamond_bvh_aa4_glass": ("blueDiamond", dict(accel="bvh", res=(160, 120), spp=4), {}),
     "assignment1_grid_aa4_glass": ("assignment1", dict(res=(128, 128), spp=4), {}),
+    # balls_high has no glass: its AA frame is a mixed-primitive two-pass frame with the wavefront replay
+    "balls_high_bvh_aa16_mixed": ("balls_high", dict(accel="bvh", res=(192, 192), spp=16), {}),
 }
+TREE_CASES = ("dragon_assignment1_bvh_aa16_glass", "assignment1_grid_aa4_glass")
 
 
 @pytest.fixture(scope="module")
@@ -80,6 +85,19 @@ def test_shipped_scene_matches_oracle(drt, oracle_mod, renderer, tmp_path, case)
     assert_same_work(a.info().accel, renderer.stats(), rst)
     if shipped.env(name):  # the sky, not bclr, fills the misses
         assert a.info().skybox_loaded
+
+
+@pytest.mark.parametrize("case", TREE_CASES + ("balls_high_bvh_aa16_mixed", "blueDiamond_bvh_aa4_glass"))
+def test_shipped_aa_frame_plans(drt, renderer, tmp_path, case):
+    """The glass cases above take the tree two-pass frame (two passes, no wavefront: the closest hits
+    of a refracting scene form a tree, MODE_TCHAIN + MODE_TREPLAY); balls_high's takes the wavefront;
+    blueDiamond (178 objects) one pass."""
+    name, over, kw = SCENE_CASES[case]
+    p = shipped.write(tmp_path, name, **over)
+    renderer.upload(drt.Scene.load_p3f(p, skybox_faces=shipped.skybox_faces(name)))
+    plan = renderer.plan(renderer.frame_params(seed=2718, **kw))
+    assert plan["passes"] == (1 if case.startswith("blueDiamond") else 2)
+    assert plan["wavefront"] == (1 if case == "balls_high_bvh_aa16_mixed" else 0)
 
 
 def test_dragon_assignment1_traversal_count_matches_reference_run(drt, renderer, tmp_path):

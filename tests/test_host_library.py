@@ -144,6 +144,18 @@ def test_p3f_parse_of_100k_triangles_is_fast_and_matches_oracle(oracle_mod, tmp_
     print(f"P3F parse of 100k triangles: {parse_s:.2f} s")
 
 
+def test_survey_synthetic_scene_bvh_has_the_reference_run_node_count():
+    """Reference pin: the reference's BVH over the survey's 100k-triangle
+    soup + floor has 118 983 nodes.  The soup is the survey's generator as reconstructed by
+    tools/generator_search.py (scenegen.survey_triangles); the product's build must give that count."""
+    s = drt.Scene()
+    s.set_accel("bvh")
+    s.add_material((1, 0.9, 0.7), 0.5, (1, 1, 1), 0.5, 30.0827, 0, 1)
+    s.add_triangles(np.concatenate([sg.survey_triangles(100_000), sg.FLOOR]))
+    s.build()
+    assert s.info().bvh_nodes == 118_983
+
+
 def test_cluster_scene_has_oversized_leaf_matching_oracle(oracle_mod, tmp_path):
     """The `cluster` scene of the GPU big-leaf cases really yields a leaf of >= 31 objects
     (the count-31 descriptor path), in the same tree as the oracle's build."""
