@@ -100,7 +100,7 @@ struct drt_ctx {
   // 4-ary shadow tree collapsed from the BVH (drt_layout.hpp); absent for a leaf root, a tree too
   // deep for the shadow stack, coordinates no record can quantise, or DRT_WIDE_SHADOW=0
   bool has_wide = false;
-  DevBuf d_wnodes, d_wleaf;  // the shadow tree's 48-B records (nodes + leaf copies), leaf box per record
+  DevBuf d_wnodes, d_wleaf;
   uint32_t wroot = 0, n_wide = 0;
   // grid
   bool has_grid = false;
@@ -295,19 +295,13 @@ static bool wide_tree_valid(const drt_bvh_node* nodes, uint32_t n_nodes, uint32_
   return leaf_objs == n_obj;
 }
 
-// Collapse the reference's binary tree into 4-ary records (drt_layout.hpp): a wide node's children are its
-// binary node's two children, the inner one with the largest box surface replaced by its two children
-// until there are four (or only leaves).  One array of 48-B records: the root's node record first, then
-// per wide node (depth-first) its block — its inner children's node records, then its leaf children's
-// primitives (copies of `prims`, the records in BVH object order; q2.w = 1 while the leaf continues),
-// leaves by ascending count so that the block's offsets stay small — and per record index the exact
-// reference leaf box of a copied primitive (`lbox`).  False if a record cannot be quantised, a block
-// offset passes kWideMaxOffset (two oversized leaves under one wide node) or 3 * depth would overflow
-// the shadow stack; the scene then keeps the binary tree for its shadow queries.
-static bool build_wide(const drt_bvh_node* nodes, const std::vector<PrimRecord>& prims, std::vector<PrimRecord>& out,
-                       std::vector<LeafBoxRecord>& lbox, uint32_t& root) {
+// Collapse the reference's binary tree (nodes, leaf descriptors per node) into 4-ary records: a
+// wide node's children are its binary node's two children, the inner one with the largest box
+// surface replaced by its two children until there are four (or only leaves).  Records in depth-
+// first order.  False if a record cannot be quantised or 3 * depth would overflow the shadow stack.
+static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& leaf_descs,
+                       std::vector<WideNodeRecord>& out, uint32_t& root) {
   out.clear();
-  lbox.clear();
   if (nodes[0].leaf) return false;
   auto area = [&](uint32_t i) {
     const drt_bvh_node& nd = nodes[i];
@@ -321,10 +315,7 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<PrimRecord>&
   };
   std::vector<Item> st{{0u, 0u, 1}};
   const int order = env_int("DRT_WIDE_ORDER", 2);
-  out.reserve(prims.size() + prims.size() / 2 + 1);
   out.emplace_back();
-  lbox.reserve(out.capacity() + 2);
-  lbox.emplace_back();  // a node record's entry stays zero
   int maxd = 1;
   while (!st.empty()) {
     const Item it = st.back();
@@ -347,11 +338,6 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<PrimRecord>&
       ch[best] = nodes[c].index;
       ch[n++] = nodes[c].index + 1;
     }
-    // a leaf without objects can never report a hit: its slot stays unused (an inverted box)
-    int m = 0;
-    for (int k = 0; k < n; k++)
-      if (!nodes[ch[k]].leaf || nodes[ch[k]].n_objs > 0) ch[m++] = ch[k];
-    n = m;
     // child slot order: the device enters the first hit slot, then the others in slot order.  Default
     // 2, ascending box surface (0: as collapsed, 1: descending, 3: leaves first, then descending)
     if (order == 1 || order == 2 || order == 3) {
@@ -363,55 +349,27 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<PrimRecord>&
     WideNodeRecord r{};
     for (int a = 0; a < 3; a++) {
       double lo[4], hi[4];
-      lo[0] = hi[0] = 0.0;
       for (int k = 0; k < n; k++) {
         lo[k] = nodes[ch[k]].bmin[a];
         hi[k] = nodes[ch[k]].bmax[a];
       }
       uint32_t e = 0;
-      if (!quantize_axis(lo, hi, std::max(n, 1), r.p[a], e, r.q[2 * a], r.q[2 * a + 1])) return false;
+      if (!quantize_axis(lo, hi, n, r.p[a], e, r.q[2 * a], r.q[2 * a + 1])) return false;
       r.ebits |= e << (8 * a);
     }
-    if (n == 0) {  // (every child an empty leaf) no slot is hit
-      for (int a = 0; a < 3; a++) r.q[2 * a] = 0xffffffffu, r.q[2 * a + 1] = 0u;
-    }
-    // the block: inner children in slot order, then the leaves' primitives by ascending count
-    const uint32_t base = (uint32_t)out.size();
-    r.base = base;
-    int inner[4], leaves[4], ni = 0, nl = 0;
-    for (int k = 0; k < n; k++) (nodes[ch[k]].leaf ? leaves[nl++] : inner[ni++]) = k;
-    std::stable_sort(leaves, leaves + nl, [&](int a, int b) { return nodes[ch[a]].n_objs < nodes[ch[b]].n_objs; });
-    uint32_t off = 0;
-    for (int j = 0; j < ni; j++) {
-      r.offs |= off << (8 * inner[j]);
-      out.emplace_back();
-      lbox.emplace_back();
-      off++;
-    }
-    for (int j = 0; j < nl; j++) {
-      const int k = leaves[j];
-      if (off > kWideMaxOffset) return false;
-      const drt_bvh_node& nd = nodes[ch[k]];
-      r.offs |= off << (8 * k);
-      r.ebits |= 1u << (24 + k);
-      LeafBoxRecord b{};
-      memcpy(b.box, nd.bmin, 12);
-      memcpy(b.box + 3, nd.bmax, 12);
-      for (uint32_t i = 0; i < nd.n_objs; i++) {
-        PrimRecord pr = prims[nd.index + i];
-        pr.q[11] = bits_as_float(i + 1 < nd.n_objs ? 1u : 0u);
-        out.push_back(pr);
-        lbox.push_back(b);
+    // children pushed in reverse so the first child's subtree follows its parent in memory
+    for (int k = n - 1; k >= 0; k--) {
+      if (nodes[ch[k]].leaf) {
+        r.desc[k] = leaf_descs[ch[k]];
+      } else {
+        r.desc[k] = (uint32_t)out.size();
+        out.emplace_back();
+        st.push_back({ch[k], r.desc[k], it.depth + 1});
       }
-      off += nd.n_objs;
     }
-    if ((uint64_t)out.size() >= 0x7fffffffull) return false;
-    memcpy(&out[it.slot], &r, sizeof(r));
-    // children pushed in reverse, so that the first inner child's block follows this one
-    for (int j = ni - 1; j >= 0; j--) st.push_back({ch[inner[j]], base + (uint32_t)j, it.depth + 1});
+    out[it.slot] = r;
   }
   if (3 * maxd > kWideMaxStack) return false;
-  lbox.resize(out.size() + 2);  // (+ 2: zeroed tail records for the node step's slot reads)
   root = 0;
   return true;
 }
@@ -681,16 +639,23 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
     r.desc[1] = dsc[nodes[i].index + 1];
     r.desc[2] = r.desc[3] = 0;
   }
-  // primitive records in BVH object order: every leaf is one contiguous run
-  std::vector<PrimRecord> perm(n_obj);
-  for (uint32_t i = 0; i < n_obj; i++) perm[i] = c->prims_scene[order[i]];
-  // 4-ary shadow tree: wide nodes and leaf-primitive copies in one 48-B record array, and the exact
-  // reference leaf box per record (DRT_WIDE_SHADOW=0: none)
-  std::vector<PrimRecord> wide;
-  std::vector<LeafBoxRecord> lbox;
+  // 4-ary shadow tree and the exact reference leaf box of every primitive (DRT_WIDE_SHADOW=0: none)
+  std::vector<WideNodeRecord> wide;
   uint32_t wroot = 0;
   const bool has_wide = env_int("DRT_WIDE_SHADOW", 1) != 0 && wide_tree_valid(nodes, n_nodes, n_obj) &&
-                        build_wide(nodes, perm, wide, lbox, wroot);
+                        build_wide(nodes, dsc, wide, wroot);
+  std::vector<LeafBoxRecord> lbox;
+  if (has_wide) {
+    lbox.assign((size_t)n_obj + 2, LeafBoxRecord{});  // + 2: the node step's tail slot reads
+    for (uint32_t i = 0; i < n_nodes; i++) {
+      const drt_bvh_node& nd = nodes[i];
+      if (!nd.leaf) continue;
+      LeafBoxRecord b{};
+      memcpy(b.box, nd.bmin, 12);
+      memcpy(b.box + 3, nd.bmax, 12);
+      for (uint32_t k = 0; k < nd.n_objs; k++) lbox[nd.index + k] = b;
+    }
+  }
   // depth (= bound on the traversal stack), iterative
   int maxd = 0;
   {
@@ -715,9 +680,8 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
   if (!recs.empty()) DRT_HIP(c, hipMemcpy(c->d_nodes.p, recs.data(), sizeof(NodeRecord) * recs.size(), hipMemcpyHostToDevice));
   c->has_wide = false;
   if (has_wide) {
-    wide.resize(wide.size() + 2);  // zeroed tail records (slot reads past a block's last record)
-    DRT_HIP(c, c->d_wnodes.ensure(sizeof(PrimRecord) * wide.size()));
-    DRT_HIP(c, hipMemcpy(c->d_wnodes.p, wide.data(), sizeof(PrimRecord) * wide.size(), hipMemcpyHostToDevice));
+    DRT_HIP(c, c->d_wnodes.ensure(sizeof(WideNodeRecord) * wide.size()));
+    DRT_HIP(c, hipMemcpy(c->d_wnodes.p, wide.data(), sizeof(WideNodeRecord) * wide.size(), hipMemcpyHostToDevice));
     DRT_HIP(c, c->d_wleaf.ensure(sizeof(LeafBoxRecord) * lbox.size()));
     DRT_HIP(c, hipMemcpy(c->d_wleaf.p, lbox.data(), sizeof(LeafBoxRecord) * lbox.size(), hipMemcpyHostToDevice));
     c->wroot = wroot;
@@ -726,6 +690,9 @@ int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, cons
   }
   DRT_HIP(c, c->d_big.ensure(sizeof(uint2) * std::max<size_t>(1, big.size())));
   if (!big.empty()) DRT_HIP(c, hipMemcpy(c->d_big.p, big.data(), sizeof(uint2) * big.size(), hipMemcpyHostToDevice));
+  // primitive records in BVH object order: every leaf is one contiguous run
+  std::vector<PrimRecord> perm(n_obj);
+  for (uint32_t i = 0; i < n_obj; i++) perm[i] = c->prims_scene[order[i]];
   DRT_HIP(c, hipMemcpy(c->d_prims.p, perm.data(), sizeof(PrimRecord) * perm.size(), hipMemcpyHostToDevice));
   c->has_bvh = true;
   c->has_grid = false;

@@ -1218,21 +1218,18 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   const bool verify = WIDE && visit && (fl & LF_VERIFY) != 0u;
   const bool inner = visit && !verify && !desc_is_leaf(cur);
   const bool leaf = visit && !verify && desc_is_leaf(cur);
-  // a shadow-tree lane's leaf is the record of its next primitive in the shadow tree's array, tested one
-  // per step whatever LEAF1 is (the record's q2.w says whether the leaf goes on; drt_layout.hpp)
-  uint32_t first = wide ? (cur & ~kLeafBit) : desc_first(cur), cnt = wide ? 1u : desc_count(cur);
-  const bool big = leaf && !wide && cnt == kBigLeaf;
+  uint32_t first = desc_first(cur), cnt = desc_count(cur);
+  const bool big = leaf && cnt == kBigLeaf;
   // LEAF1 1 / 2: one primitive of a leaf per step (below), 2 also leaving the last slot unread for
   // such a step; 0: the whole leaf in the step
-  const bool whole = !wide && (LEAF1 == 0 || big);
+  const bool whole = LEAF1 == 0 || big;
   if (big) {  // oversized leaf: (first, count) from the side table
     const uint2 bl = S.big_leaves[first];
     first = bl.x;
     cnt = bl.y;
   }
-  // (a shadow-tree record is 48 B, node or primitive copy; a leaf-box check reads 32 B)
-  const float4* rec = verify ? S.wleaf + 2 * (size_t)cur
-                             : (wide ? S.wnodes + 3 * (size_t)first : (leaf ? S.prims + 3 * (size_t)first : S.nodes + 4 * (size_t)cur));
+  const float4* rec = leaf ? S.prims + 3 * (size_t)first
+                           : (verify ? S.wleaf + 2 * (size_t)cur : (wide ? S.wnodes : S.nodes) + 4 * (size_t)cur);
   float4 s0, s1, s2, s3, s4, s5;
   bool uni_done = false;
   if (UNI && visit) {
@@ -1255,15 +1252,13 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   if (visit && !uni_done) {
     s0 = rec[0];
     s1 = rec[1];
-    if (!(WIDE && verify)) s2 = rec[2];  // (a leaf box is two slots)
+    s2 = rec[2];
     // (Measured alternative, kept out: an 8-B load of the last slot for inner nodes, which use
     // only its two child descriptors: the split into two masked loads cost 8.6 %.)
     // The last slot serves inner nodes (child descriptors) and whole-leaf steps (the second
     // primitive's first slot); a one-primitive leaf step does not read it (LEAF1 2: +1.3 % on the
     // headline; the closest-chain pass of in-order frames lost 1.5 % with it and keeps 1).
-    // A shadow-tree lane never reads a fourth slot (round 6: its records are 48 B, so a shadow step issues
-    // three loads where the 64-B records of rounds 4-5 took four).
-    if ((LEAF1 != 2 || inner || whole) && !wide) s3 = rec[3];
+    if (LEAF1 != 2 || inner || whole) s3 = rec[3];
   }
   if (leaf && whole && cnt > 1) {
     s4 = rec[4];
@@ -1290,11 +1285,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     const bool px = L.q.sx(), py = L.q.sy(), pz = L.q.sz();
     const uint32_t nx = px ? lx : hx, fx = px ? hx : lx, ny = py ? ly : hy, fy = py ? hy : ly, nz = pz ? lz : hz,
                    fz = pz ? hz : lz;
-    // child k: record base + byte k of offs, a leaf (its first primitive's record) if bit 24 + k of s0.w is set
-    const uint32_t base = __float_as_uint(s2.z), offs = __float_as_uint(s2.w);
-    uint32_t d[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = (base + ((offs >> (8 * k)) & 0xffu)) | (((eb >> (24 + k)) & 1u) << 31);
+    const uint32_t d[4] = {__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w)};
     float tn[4];
     bool hk[4];
 #ifdef DRT_WIDE_PK
@@ -1503,8 +1494,8 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     // four loads fetch it with the other lanes' nodes: the rest of the leaf is itself a leaf
     // descriptor.  (The second primitive's two slots loaded beside the first, for the few lanes
     // with such a leaf, cost a load instruction each at a per-instruction floor: tools/td_lanes.hip.)
-    const bool more = wide ? !done && __float_as_uint(s2.w) != 0u : !whole && !done && cnt > 1;
-    if (more) L.cur = wide ? (kLeafBit | (first + 1u)) : leaf_desc(first + 1, cnt - 1);
+    const bool more = !whole && !done && cnt > 1;
+    if (more) L.cur = leaf_desc(first + 1, cnt - 1);
     fl = more ? (fl | LF_LEAFCONT) : (fl & ~LF_LEAFCONT);
     if (!more && (fl & LF_TRAV) && !(WIDE && (fl & LF_VERIFY))) fl |= LF_POP;
   }
@@ -1926,6 +1917,31 @@ __device__ __forceinline__ bool wf_pair_used(const SceneArgs& S, const FrameArgs
   return m == 1 || j % m == 0 || S.lights[j / m].type == DRT_LIGHT_QUAD;
 }
 
+// The wavefront's streaming buffers (query records, Phong factors, level records, answers) are written
+// once and read once, between uses of the tree records.  -DDRT_WF_NT (A/B) moves them
+// with non-temporal stores and loads, so that they do not displace tree records from the caches.
+#ifdef DRT_WF_NT
+typedef float wf_f4 __attribute__((ext_vector_type(4)));
+typedef float wf_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void wf_st(float4* p, float4 v) { __builtin_nontemporal_store(wf_f4{v.x, v.y, v.z, v.w}, (wf_f4*)p); }
+__device__ __forceinline__ void wf_st(float2* p, float2 v) { __builtin_nontemporal_store(wf_f2{v.x, v.y}, (wf_f2*)p); }
+__device__ __forceinline__ void wf_st(uint8_t* p, uint8_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ float4 wf_ld(const float4* p) {
+  const wf_f4 v = __builtin_nontemporal_load((const wf_f4*)p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float2 wf_ld(const float2* p) {
+  const wf_f2 v = __builtin_nontemporal_load((const wf_f2*)p);
+  return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ uint8_t wf_ld(const uint8_t* p) { return __builtin_nontemporal_load(p); }
+#else
+template <class T>
+__device__ __forceinline__ void wf_st(T* p, T v) { *p = v; }
+template <class T>
+__device__ __forceinline__ T wf_ld(const T* p) { return *p; }
+#endif
+
 // Query slot of (level l, pair u, chunk slot s): [band][level][pair][slot in band], a band being W.band
 // consecutive sample slots, so that band b's queries are one contiguous range (the streaming kernels
 // give XCD b that range first: its L2 then serves the rays of one screen band)
@@ -1942,7 +1958,7 @@ __device__ bool wf_level(const SceneArgs& S, const FrameArgs& F, const WfArgs& W
   const size_t li_ = (size_t)l * W.n_slots + slot;
   if (!hit) {  // main.cpp:351-357
     const V3 c = cclamp(background(S, q.d));
-    W.lvl[li_] = make_float4(c.x, c.y, c.z, __uint_as_float(WF_MISS << 24));
+    wf_st(&W.lvl[li_], make_float4(c.x, c.y, c.z, __uint_as_float(WF_MISS << 24)));
     return false;
   }
   const V3 hitP = add(q.o, mul(q.d, t));
@@ -1966,9 +1982,9 @@ __device__ bool wf_level(const SceneArgs& S, const FrameArgs& F, const WfArgs& W
     // BVH::Traverse(Ray&) normalises Ls, range |Ls| + EPSILON; Grid::Traverse(Ray&) gets the unit L,
     // range |L|, direction re-normalised (Q1; setup_shadow)
     const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
-    W.rays[qi] = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
-    W.rays_b[qi] = make_float4(sd.x, sd.y, sd.z, 0.0f);
-    W.nl[qi] = make_float2(NdotL, NdotH);
+    wf_st(&W.rays[qi], make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls))));
+    wf_st(&W.rays_b[qi], make_float4(sd.x, sd.y, sd.z, 0.0f));
+    wf_st(&W.nl[qi], make_float2(NdotL, NdotH));
   }
   uint32_t flags = 0u;
   bool more = false;
@@ -1998,14 +2014,14 @@ __device__ bool wf_level(const SceneArgs& S, const FrameArgs& F, const WfArgs& W
       more = true;
     }
   }
-  W.lvl[li_] = make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24)));
+  wf_st(&W.lvl[li_], make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24))));
   return more;
 }
 // No shadow query at levels from..max_depth of chunk slot `slot` (past its chain's end; a miss level
 // has none either).
 __device__ __forceinline__ void wf_mark_empty(const WfArgs& W, int from, uint32_t slot) {
   for (int k = from; k < W.levels; k++)
-    for (int j = 0; j < W.pairs; j++) W.rays[wf_q(W, k, j, slot)] = make_float4(0.f, 0.f, 0.f, -1.0f);
+    for (int j = 0; j < W.pairs; j++) wf_st(&W.rays[wf_q(W, k, j, slot)], make_float4(0.f, 0.f, 0.f, -1.0f));
 }
 
 // MODE_SKEL: the closest query of bounce L.depth of sample L.smp returned: record it.  A hit that
@@ -2149,12 +2165,12 @@ __device__ __forceinline__ void lane_init(const SceneArgs& S, const FrameArgs& F
     return;
   }
   if (MODE == MODE_QSTREAM) {  // work item = one shadow query of a wavefront replay
-    const float4 a = F.q_rays[item];
+    const float4 a = wf_ld(&F.q_rays[item]);
     if (a.w < 0.0f) {  // an empty slot: no query
       L.item = kNoItem;
       return;
     }
-    const float4 b = F.q_rays_b[item];
+    const float4 b = wf_ld(&F.q_rays_b[item]);
     L.fl = 0u;
     start_query<STATS, ACC>(S, L, make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)), true, a.w, C);
     return;
@@ -2419,7 +2435,7 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
       if (done) {
         if (MODE == MODE_SEQ && part == kPartYield) L.fl |= LF_YIELD;
         if constexpr (MODE == MODE_QSTREAM) {  // the query's answer (a Grid miss of the grid box: shadowed)
-          F.q_occ[L.item] = (L.fl & LF_HIT) ? 1 : 0;
+          wf_st(&F.q_occ[L.item], (uint8_t)((L.fl & LF_HIT) ? 1 : 0));
           L.item = kNoItem;
         } else if constexpr (MODE == MODE_SKEL) skel_process<STATS, ACC>(S, F, L, C);
         else if constexpr (MODE == MODE_CHAIN) chain_process<STATS, ACC>(S, F, L, C);
@@ -2518,11 +2534,11 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
         if (it < chunk_end) {
           // (interleaved records: rays_b = rays + 1, stride 2; or two arrays, stride 1)
           const size_t at = (size_t)it * (uint32_t)A.stride;
-          const float4 a = A.rays[at];
+          const float4 a = wf_ld(&A.rays[at]);
           // (an empty slot is thr < 0, wf_mark_empty; a NaN range is a query, answered 0, as MODE_QSTREAM
           // answers it — ADVICE r5: skipping it left a stale answer in occ_out)
           if (!A.sparse || !(a.w < 0.0f)) {
-          const float4 b = A.rays_b[at];
+          const float4 b = wf_ld(&A.rays_b[at]);
           L.item = it;
           L.q = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
           L.thr = a.w;
@@ -2565,7 +2581,7 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
     }
     if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
       if (KIND == 2) {
-        A.occ_out[L.item] = (L.fl & LF_HIT) ? 1 : 0;
+        wf_st(&A.occ_out[L.item], (uint8_t)((L.fl & LF_HIT) ? 1 : 0));
       } else {
         const bool hit = (L.fl & LF_HIT) != 0u;
         A.t_out[L.item] = hit ? L.best_t : 3.402823466e+38f;
@@ -2653,12 +2669,12 @@ __device__ __forceinline__ V3 wf_sample(const SceneArgs& S, const FrameArgs& F, 
   // the last level of the chain: a miss, the depth cut, or a hit without a mirror child
   int last = 0;
   for (; last < md; last++) {
-    const uint32_t fl = __float_as_uint(W.lvl[(size_t)last * ns + slot].w) >> 24;
+    const uint32_t fl = __float_as_uint(wf_ld(&W.lvl[(size_t)last * ns + slot]).w) >> 24;
     if (!(fl & WF_REFL)) break;
   }
   V3 c = mk(0, 0, 0);
   for (int l = last; l >= 0; l--) {
-    const float4 rv = W.lvl[(size_t)l * ns + slot];
+    const float4 rv = wf_ld(&W.lvl[(size_t)l * ns + slot]);
     const uint32_t w = __float_as_uint(rv.w), flags = w >> 24, mat = w & 0xffffffu;
     if (flags & WF_MISS) {
       c = mk(rv.x, rv.y, rv.z);
@@ -2669,8 +2685,8 @@ __device__ __forceinline__ V3 wf_sample(const SceneArgs& S, const FrameArgs& F, 
     for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // main.cpp:444-450, in the light loop's order
       if (!wf_pair_used(S, F, j)) continue;
       const size_t qi = wf_q(W, l, u++, slot);
-      if (W.occ[qi]) continue;
-      const float2 nl = W.nl[qi];
+      if (wf_ld(&W.occ[qi])) continue;
+      const float2 nl = wf_ld(&W.nl[qi]);
       acc = add(acc, light_term(m, nl.x, nl.y, S.lights[light_of_pair(j, F)], F));
     }
     if (flags & WF_DEEP) {

@@ -22,24 +22,19 @@
 // (bit 31 set): bits 0..25 = first primitive, bits 26..30 = object count (< 31); count 31
 // marks an oversized leaf whose (first, count) pair lives in the big-leaf table at bits 0..25.
 //
-// Shadow tree (round 4; 48-B records since round 6): BVH::Traverse(Ray&) (bvh.cpp:316-391) answers "is
-// any primitive of a leaf whose box the ray hits within range" — an any-hit boolean whose value does not
-// depend on the visit order.  Shadow queries of finite rays therefore walk a 4-ary tree collapsed from
-// the reference's binary tree (same leaves), stored as ONE array of 48-B records (three 16-B slots, so a
-// shadow step issues three loads, not four) holding both the wide nodes and a copy of the leaves'
-// primitives.  Each wide node owns a block of consecutive records starting at `base`: its inner
-// children's node records, then its leaf children's primitives (each leaf a run, in its reference order):
-//   s0 = (p.x, p.y, p.z, bits: E.x | E.y << 8 | E.z << 16 | leafmask << 24)   anchor, exponents, leaf bits
-//   s1 = (lo.x, hi.x, lo.y, hi.y)   s2 = (lo.z, hi.z, base, offs)   one byte per child per dword
-// Child k is the record base + byte k of offs, a leaf's first primitive if bit k of leafmask is set.
+// Shadow tree (round 4): BVH::Traverse(Ray&) (bvh.cpp:316-391) answers "is any primitive of a
+// leaf whose box the ray hits within range" — an any-hit boolean whose value does not depend on
+// the visit order.  Shadow queries of finite rays therefore walk a 4-ary tree collapsed from the
+// reference's binary tree (same leaves), 64 B per node = the four 16-B slots the node step loads:
+//   s0 = (p.x, p.y, p.z, bits: E.x | E.y << 8 | E.z << 16)   anchor and biased exponents
+//   s1 = (lo.x, hi.x, lo.y, hi.y)   s2 = (lo.z, hi.z, 0, 0)   one byte per child per dword
+//   s3 = (desc[0], desc[1], desc[2], desc[3])                 inner wide index or leaf descriptor
 // Child k's box on axis a is [p.a + lo.a[k] * 2^(E.a-127), p.a + hi.a[k] * 2^(E.a-127)]: p.a is a
 // multiple of the scale, so every decoded plane is an exact float (one FMA, no rounding) and the
 // box contains the child's reference box.  An unused child slot has lo = 255, hi = 0: an inverted
-// box that no ray hits.  A copied primitive is the 48-B primitive record with q2.w = 1 when the next
-// record continues its leaf (0 at the leaf's last primitive): a lane tests one primitive per step.
-// A primitive hit within range is accepted only after the exact box of its reference leaf (the leaf-box
-// array, 32 B per record index: (min.xyz, max.x), (max.yz, 0, 0)) is hit too, so the accepted set is
-// exactly the reference's ("shadow tree").
+// box that no ray hits.  A primitive hit within range is accepted only after the exact box of its
+// reference leaf (wide leaf-box array, 32 B per primitive: (min.xyz, max.x), (max.yz, 0, 0)) is
+// hit too, so the accepted set is exactly the reference's ("shadow tree").
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -77,19 +72,18 @@ struct NodeRecord {
 };
 struct WideNodeRecord {
   float p[3];
-  uint32_t ebits;  // E.x | E.y << 8 | E.z << 16 | leafmask << 24
-  uint32_t q[6];   // lo.x, hi.x, lo.y, hi.y, lo.z, hi.z (byte k = child k)
-  uint32_t base;   // the node's block: its first child record
-  uint32_t offs;   // byte k: child k's record - base
+  uint32_t ebits;
+  uint32_t q[6];  // lo.x, hi.x, lo.y, hi.y, lo.z, hi.z (byte k = child k)
+  uint32_t pad[2];
+  uint32_t desc[4];
 };
-constexpr uint32_t kWideMaxOffset = 255u;  // a block's children within 256 records of its base
 struct LeafBoxRecord {
   float box[6];
   uint32_t pad[2];
 };
 static_assert(sizeof(PrimRecord) == 48, "prim record is 48 B");
 static_assert(sizeof(NodeRecord) == 64, "node record is 64 B");
-static_assert(sizeof(WideNodeRecord) == 48, "wide node record is 48 B");
+static_assert(sizeof(WideNodeRecord) == 64, "wide node record is 64 B");
 static_assert(sizeof(LeafBoxRecord) == 32, "leaf box record is 32 B");
 
 inline float bits_as_float(uint32_t u) {

@@ -32,9 +32,7 @@ BUDGET = {
     # C4 as two passes (round 3): the closest-chain pass, and the per-sample replay without refraction
     # (round 5: its frame heads in lane-contiguous global memory, not scratch: 2 224 -> 880 B)
     "drt::path_persistent<true, false, 5, 6, 2>": (80, 704, 6, 5),
-    # (round 6: 53 spills — its shadow-tree lanes test one leaf primitive per step on the 48-B records; the
-    # persistent replay runs only with DRT_WAVEFRONT=0 or when the wavefront's buffers do not fit)
-    "drt::path_persistent<true, false, 6, 6, 2>": (80, 880, 6, 53),
+    "drt::path_persistent<true, false, 6, 6, 2>": (80, 880, 6, 39),
     # round 4: the headline's AA frame in two passes — its closest-chain pass, and (round 5: its own
     # instantiation, MODE_AREPLAY, no RNG code: 45 -> 35 spills) its replay pass
     "drt::path_persistent<true, false, 7, 6, 2>": (80, 704, 6, 2),
@@ -44,10 +42,9 @@ BUDGET = {
     # batched shadow queries (drt_trace_shadow) on the 4-ary shadow tree: 8 waves/SIMD, no spills
     # (round 5: 64 VGPRs with the two-array query records (TraceArgs::stride): 7 waves by the compiler's
     # count, down from 8)
-    # (round 6: 48-B shadow-tree records, child records decoded from a base + byte offsets: 68 VGPRs, 7 waves)
-    "drt::trace_stream<true, 2, 6, false>": (72, 352, 7, 0),
+    "drt::trace_stream<true, 2, 6, false>": (64, 352, 7, 0),
     # the wavefront replay's shadow queries (round 5): 7 waves/SIMD of LDS stack, no spills
-    "drt::trace_stream<true, 2, 7, false>": (72, 352, 7, 0),
+    "drt::trace_stream<true, 2, 7, false>": (64, 352, 7, 0),
     # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs), and the two passes of the Grid headline's frame
     "drt::path_persistent<true, false, 0, 5, 1>": (96, 1844, 5, 79),
     "drt::path_persistent<true, false, 7, 5, 1>": (96, 8, 5, 1),
