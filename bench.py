@@ -200,8 +200,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-load-timing", action="store_true",
                     help="skip the P3F leg: the synthetic scene written as a .p3f file (by a child process "
-                         "while the GPU runs) and parsed + built after the timed region (f1: Scene::load_p3f "
-                         "+ BVH::Build, scene.cpp:565-594, bvh.cpp:27-227)")
+                         "during the scene build and the stats frames, waited for before the timed frames) and "
+                         "parsed + built after the timed region (f1: Scene::load_p3f + BVH::Build, "
+                         "scene.cpp:565-594, bvh.cpp:27-227)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -212,8 +213,9 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    # f1 leg: the same scene as a P3F file, written by a child process while the GPU works (np.savetxt
-    # of 3M vertices takes ~10 s of one core), parsed and built after the timed region
+    # f1 leg: the same scene as a P3F file, written by a child process during the scene build and the stats
+    # frames (np.savetxt of 3M vertices takes ~10 s of one core), waited for before the settle frames, and
+    # parsed and built after the timed region
     p3f_writer, p3f_path = None, None
     # Started before anything touches the GPU, and not under a profiler (rocprofv3 preloads its
     # library into every child, and with --pmc that library would initialise the GPU in the writer).
@@ -328,6 +330,17 @@ def main():
     mine = dict(zip(keys, mine.tolist()))
     rays_frame = tot["closest_rays"] + tot["shadow_rays"]
 
+    # the f1 leg's P3F writer (one core, ~10 s at 1M triangles) finishes before the settle, warmup and
+    # timed frames, so that nothing else of this run shares the host while they run
+    p3f_wait_s = 0.0
+    if p3f_writer is not None:
+        t_w = time.perf_counter()
+        try:
+            p3f_writer.wait(timeout=300)
+        except Exception:  # noqa: BLE001 (the f1 leg reports the failure below)
+            pass
+        p3f_wait_s = time.perf_counter() - t_w
+        log(f"[bench] waited {p3f_wait_s:.1f} s for the P3F writer before the timed frames")
     # clock settle: as many untimed frames as fill --settle-s (one frame timed first; the count is
     # the max over ranks, since every frame of a multi-rank run holds a collective)
     settle = 0
@@ -584,6 +597,7 @@ def main():
             same = fs.info().n_objects == info.n_objects and fs.info().bvh_nodes == info.bvh_nodes
             out["load"] = {"p3f_bytes": drt_scene_bytes, "parse_s": round(parse_s, 2), "build_s": round(fbuild_s, 2),
                            "load_build_s": round(parse_s + fbuild_s, 2), "same_scene": bool(same),
+                           "writer_wait_s": round(p3f_wait_s, 1),
                            "note": "setup_s builds from in-memory triangles; this is the P3F file path"}
             log(f"[bench] P3F {drt_scene_bytes / 1e6:.0f} MB: parse {parse_s:.2f} s, BVH build {fbuild_s:.2f} s")
             del fs

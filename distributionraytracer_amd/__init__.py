@@ -348,6 +348,17 @@ class Renderer:
             check(n, self.h, "drt_frame_pass_times")
         return np.array(a[:n]), np.array(b[:n])
 
+    def wave_times(self, pass_index=0, max_waves=1 << 14):
+        """Per resident wave of the last stats frame's persistent launch (pass 0 or 1): (start, end)
+        s_memrealtime stamps in us (100 MHz clock), rows of waves that ran; (drt_frame_wave_times)."""
+        buf = (C.c_uint64 * (2 * max_waves))()
+        n = _lib.load().drt_frame_wave_times(self.h, pass_index, buf, max_waves)
+        if n < 0:
+            check(n, self.h, "drt_frame_wave_times")
+        a = np.frombuffer(buf, dtype=np.uint64, count=2 * n).reshape(n, 2)
+        a = a[(a[:, 0] > 0) & (a[:, 1] > 0)]
+        return a.astype(np.float64) / 100.0
+
     def frame_spans(self, max_frames=512):
         """(path start, path end, frame end) of recent frames in ms on one device clock, from the
         oldest frame's path-kernel start (HIP events on each frame's stream)."""

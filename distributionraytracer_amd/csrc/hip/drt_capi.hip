@@ -101,6 +101,10 @@ struct drt_ctx {
   // deep for the shadow stack, coordinates no record can quantise, or DRT_WIDE_SHADOW=0
   bool has_wide = false;
   DevBuf d_wnodes, d_wleaf;
+  // stats frames: per resident wave of each path_persistent launch (pass 1, then pass 2) its (start, end)
+  // s_memrealtime stamps (drt_frame_wave_times); wave_slots = waves per pass
+  DevBuf d_wave_times;
+  uint32_t wave_slots = 0;
   uint32_t wroot = 0, n_wide = 0;
   // grid
   bool has_grid = false;
@@ -1226,6 +1230,14 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
   const bool stats = (p->flags & DRT_FRAME_STATS) != 0;
   c->stats_valid = stats;
   if (stats) DRT_HIP(c, hipMemsetAsync(d_stats.p, 0, sizeof(unsigned long long) * ST_COUNT, st));
+  if (stats && P.persistent) {  // per-wave start / end stamps of the persistent launches (<= 32 waves per CU)
+    if (!c->cus) DRT_HIP(c, hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    c->wave_slots = (uint32_t)std::max(1, c->cus) * 32u;
+    const size_t wt_bytes = sizeof(unsigned long long) * 2u * 2u * c->wave_slots;
+    DRT_HIP(c, c->d_wave_times.ensure(wt_bytes));
+    DRT_HIP(c, hipMemsetAsync(c->d_wave_times.p, 0, wt_bytes, st));
+    P.F.wave_times = c->d_wave_times.as<unsigned long long>();
+  }
   P.F.samples = d_samples.as<float4>();
   P.F.stats = d_stats.as<unsigned long long>();
   P.R.samples = P.F.samples;
@@ -1373,6 +1385,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F2.n_items = P.n_slots;
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     F2.work_counter = d_counter.as<unsigned int>() + 256;
+    if (F2.wave_times) F2.wave_times += 2u * c->wave_slots;  // pass 2's launches (persistent replay / MODE_QSTREAM)
     for (uint32_t k = 0; wavefront && k < P.wf_chunks; k++) {
       W.slot0 = (uint32_t)(k * P.wf_chunk);
       W.n_slots = (uint32_t)std::min<uint64_t>(P.wf_chunk, P.n_slots - W.slot0);
@@ -1559,6 +1572,19 @@ int drt_frame_pass_times(drt_ctx* c, int max_frames, double* pass1_ms, double* p
     if (pass2_ms) pass2_ms[i] = b;
   }
   return n;
+}
+
+int drt_frame_wave_times(drt_ctx* c, int pass, uint64_t* start_end, int64_t max_waves) {
+  if (!c || pass < 0 || pass > 1 || max_waves < 0 || (max_waves && !start_end)) return DRT_E_INVALID;
+  if (!c->stats_valid || !c->d_wave_times.p) DRT_FAIL(c, DRT_E_STATE, "no stats frame with wave stamps");
+  DRT_HIP(c, hipSetDevice(c->device));
+  DRT_HIP(c, hipDeviceSynchronize());
+  const int64_t n = std::min<int64_t>(max_waves, (int64_t)c->wave_slots);
+  if (n) {
+    DRT_HIP(c, hipMemcpy(start_end, c->d_wave_times.as<unsigned long long>() + 2u * c->wave_slots * (uint32_t)pass,
+                         sizeof(uint64_t) * 2u * (size_t)n, hipMemcpyDeviceToHost));
+  }
+  return (int)n;
 }
 
 int drt_frame_spans(drt_ctx* c, int max_frames, double* path_start, double* path_end, double* frame_end) {

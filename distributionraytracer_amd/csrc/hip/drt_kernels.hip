@@ -2269,6 +2269,8 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
   // within 0.3 %, and 17 more VGPR spills in the mixed-primitive AA kernel.)
   uint32_t part = __builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u, parts_done = 0;  // HW_REG_XCC_ID
   uint64_t cyc[4] = {0, 0, 0, 0};  // stats builds: refill / node / shading / leaf-block cycles (wave-uniform)
+  if (STATS && F.wave_times != nullptr && lane == 0)  // (a vector store by lane 0)
+    F.wave_times[2 * ((blockIdx.x * blockDim.x + threadIdx.x) >> 6)] = __builtin_amdgcn_s_memrealtime();
   // MODE_SEQ tail (F.seq_cont): a lane runs a whole pixel's samples in order, so once every pixel
   // is claimed the frame's last ~quarter runs on waves whose lanes finish their last pixel at
   // different times (C4 at 1024^2: 0.56 node-loop SIMD efficiency, against 0.69 at 2048^2 with
@@ -2450,6 +2452,8 @@ __global__ void __launch_bounds__(pblock<ACC>(), WAVES) path_persistent(SceneArg
     }
   }
   flush_stats<STATS>(F, C);
+  if (STATS && F.wave_times != nullptr && lane == 0)
+    F.wave_times[2 * ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) + 1] = __builtin_amdgcn_s_memrealtime();
   if (STATS && lane == 0) {
     atomicAdd(&F.stats[ST_CYC_REFILL], (unsigned long long)cyc[0]);
     atomicAdd(&F.stats[ST_CYC_NODE], (unsigned long long)cyc[1]);

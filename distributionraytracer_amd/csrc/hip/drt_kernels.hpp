@@ -210,6 +210,9 @@ struct FrameArgs {
   const float4* q_rays;    // per query: (o, range); thr < 0: no query
   const float4* q_rays_b;  // per query: (d, 0)
   uint8_t* q_occ;
+  // stats launches (STATS build of path_persistent), when set: per resident wave of this launch its
+  // (start, end) s_memrealtime stamps (100 MHz), indexed by global thread id / 64 (drt_frame_wave_times)
+  unsigned long long* wave_times;
 };
 
 // Control words of the MODE_SEQ tail in the per-frame work-counter block (1 KiB, zeroed per

@@ -293,6 +293,13 @@ int drt_frame_times(drt_ctx* ctx, int max_frames, double* path_ms, double* total
  * oldest frame returned: path-kernel start / end and frame end.  Frames on different streams
  * overlap; the union of their path-kernel spans is the device time the path kernel held. */
 int drt_frame_spans(drt_ctx* ctx, int max_frames, double* path_start, double* path_end, double* frame_end);
+
+/* Diagnostics of the last stats frame (DRT_FRAME_STATS) rendered by the persistent kernel: per resident
+ * wave of its pass-1 (pass = 0) or pass-2 (pass = 1, the persistent replay or the Grid's query stream)
+ * launch, the (start, end) s_memrealtime stamps (100 MHz) in start_end[2 * w], [2 * w + 1]; 0 = no such
+ * wave.  Returns the number of wave slots written (<= max_waves).  No reference counterpart: it measures
+ * the tail of a launch. */
+int drt_frame_wave_times(drt_ctx* ctx, int pass, uint64_t* start_end, int64_t max_waves);
 /* The same frames' passes: a two-pass frame (drt_frame_plan.passes == 2) is the closest-chain pass
  * then the replay pass, timed from the path-kernel start to the end of the first launch and from
  * there to the path-kernel end (HIP events on the frame's stream; pass1 + pass2 = path_ms of

@@ -1068,3 +1068,29 @@ def test_frame_pass_times_split_the_path_time(drt, monkeypatch):
         np.testing.assert_allclose(p1 + p2, path_ms, rtol=1e-3, atol=2e-3)
     finally:
         r.close()
+
+
+def test_frame_wave_times_cover_the_persistent_launch(drt, monkeypatch):
+    """drt_frame_wave_times (round 6, tools/launch_tail.py): a stats frame's persistent launches stamp each
+    resident wave's start and end; every wave ends after it starts, and the spans lie inside the frame."""
+    import bench
+
+    s = drt.Scene()
+    bench.populate(s, bench.synthetic_triangles(20_000), 96, 16, aperture=4.0, focal=1.0)
+    s.build()
+    r = drt.Renderer(0)
+    try:
+        r.upload(s)
+        monkeypatch.setenv("DRT_AA_TWO_PASS", "2")
+        r.render(seed=5, stats=True, max_depth=3)
+        assert r.plan(r.frame_params(seed=5, max_depth=3))["passes"] == 2
+        w = r.wave_times(0)
+        assert len(w) > 64 and (w[:, 1] >= w[:, 0]).all()
+        span_us = w[:, 1].max() - w[:, 0].min()
+        path_ms, _ = r.frame_times(1)
+        assert 0 < span_us <= path_ms[-1] * 1e3 * 1.05 + 20
+        r.render(seed=5)  # a frame without stats does not stamp
+        with pytest.raises(RuntimeError):
+            r.wave_times(0)
+    finally:
+        r.close()
