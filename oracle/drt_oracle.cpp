@@ -318,7 +318,15 @@ struct KRng {
   uint32_t seed, pix, k;
   uint32_t shift = 17;    // 15-bit draws (MSVC CRT); 1 = 31-bit draws (glibc, harness pinning only)
   int rmax = kRandMax;
-  int rand_() { uint32_t h = mix32(seed ^ mix32(pix * 0x9E3779B9u ^ mix32(k++))); return (int)(h >> shift); }
+  uint32_t* lcg = nullptr;  // orc_options.lcg: the MSVC CRT rand() state shared by the whole frame
+  int rand_() {
+    if (lcg) {  // MSVC rand(): holdrand = holdrand * 214013 + 2531011; return (holdrand >> 16) & 0x7fff
+      *lcg = *lcg * 214013u + 2531011u;
+      return (int)((*lcg >> 16) & 0x7fffu);
+    }
+    uint32_t h = mix32(seed ^ mix32(pix * 0x9E3779B9u ^ mix32(k++)));
+    return (int)(h >> shift);
+  }
   float rand_float() { return (float)((double)(float)rand_() / ((double)(float)rmax + 1.0)); }  // maths.h:80
 };
 V3 rnd_unit_disk(KRng& g) {  // maths.h:101-107
@@ -965,6 +973,14 @@ C3 orc_scene::ray_tracing(Ray ray, int depth, float ior_1, V3 lightSample, KRng&
 // ==========================================================================================
 extern "C" {
 
+// The first n draws of the CRT rand() sequence orc_options.lcg uses (MSVC: srand(seed), then rand()).
+void orc_crt_rand(uint32_t seed, int n, int32_t* out) {
+  uint32_t state = seed;
+  KRng g{0, 0, 0};
+  g.lcg = &state;
+  for (int i = 0; i < n; i++) out[i] = g.rand_();
+}
+
 uint32_t orc_keyed_rand(uint32_t seed, uint32_t pixel, uint32_t k) {
   KRng g{seed, pixel, k};
   return (uint32_t)g.rand_();
@@ -1386,6 +1402,9 @@ int orc_render(orc_scene* s, uint32_t seed, const orc_options* opt, float* rgb, 
   const long prog = opt ? opt->progressive_frame : 0;      // FrameCount of zone A, 0 = zone B
   if (prog >= 10000) return 0;                             // FrameCount == MAX_SAMPLES: no render (main.cpp:537)
   int threads = (opt && opt->threads > 0) ? opt->threads : 0;
+  const bool lcg = opt && opt->lcg;  // one CRT rand() sequence in pixel order: one thread
+  uint32_t lcg_state = lcg ? opt->lcg_seed : 0u;
+  if (lcg) threads = 1;
 #ifdef _OPENMP
   int nthr = threads > 0 ? threads : omp_get_max_threads();
 #else
@@ -1402,6 +1421,7 @@ int orc_render(orc_scene* s, uint32_t seed, const orc_options* opt, float* rgb, 
     Stats& st = tst[0];
 #endif
     KRng g{seed, (uint32_t)(y * RX + x), 0};
+    if (lcg) g.lcg = &lcg_state;
     C3 color = cmk(0, 0, 0);
     if (prog > 0) {  // zone A (main.cpp:540-586): one jittered sample, lerped into the frame
       V3 ps;

@@ -63,6 +63,11 @@ typedef struct {
   int light_spp;    /* shadow samples per quad light per hit (C3); 0/1 = reference  */
   int progressive_frame; /* 0 = zone B; n >= 1 = zone A frame FrameCount n: one sample per
                             pixel lerped into rgb (in/out) with weight 1/n (main.cpp:536-599) */
+  int lcg;          /* 1: the CRT rand() of the reference's own runs instead of the keyed stream — the
+                       MSVC LCG x = x * 214013 + 2531011, (x >> 16) & 0x7FFF, seeded with lcg_seed, one
+                       sequence through the frame in renderScene's pixel order (main.cpp:603-605), one
+                       thread (test infrastructure: reproduces the survey's reference-run counts) */
+  uint32_t lcg_seed;
 } orc_options;
 
 /* ---- scene construction ---- */
@@ -129,6 +134,8 @@ int orc_render(orc_scene*, uint32_t seed, const orc_options* opt, float* rgb /* 
 
 /* ---- keyed RNG ---- */
 uint32_t orc_keyed_rand(uint32_t seed, uint32_t pixel, uint32_t k);
+/* the CRT rand() of orc_options.lcg: the first n draws after srand(seed) */
+void orc_crt_rand(uint32_t seed, int n, int32_t* out);
 
 #ifdef __cplusplus
 }

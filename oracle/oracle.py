@@ -48,7 +48,7 @@ class OrcStats(C.Structure):
 class OrcOptions(C.Structure):
     _fields_ = [("max_depth", C.c_int), ("roughness", C.c_float), ("threads", C.c_int),
                 ("row_begin", C.c_int), ("row_end", C.c_int), ("light_spp", C.c_int),
-                ("progressive_frame", C.c_int)]
+                ("progressive_frame", C.c_int), ("lcg", C.c_int), ("lcg_seed", C.c_uint32)]
 
 
 def build(force: bool = False) -> None:
@@ -111,6 +111,8 @@ def lib():
         L.orc_render.argtypes = [vp, C.c_uint32, C.POINTER(OrcOptions), _f, C.POINTER(OrcStats)]
         L.orc_keyed_rand.restype = C.c_uint32
         L.orc_keyed_rand.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_crt_rand.restype = None
+        L.orc_crt_rand.argtypes = [C.c_uint32, C.c_int, C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 
@@ -325,11 +327,13 @@ class Scene:
         return out
 
     def render(self, seed=1, max_depth=4, roughness=0.0, threads=0, rows=None, light_spp=1, progressive_frame=0,
-               accum=None):
-        """progressive_frame n >= 1: zone A frame n, lerped into `accum` (updated in place)."""
+               accum=None, lcg_seed=None):
+        """progressive_frame n >= 1: zone A frame n, lerped into `accum` (updated in place).
+        lcg_seed: draw from the MSVC CRT rand() sequence seeded with it (one thread, pixel order) instead of
+        the keyed stream — the RNG of the survey's reference runs."""
         info = self.info()
         opt = OrcOptions(max_depth, roughness, threads, rows[0] if rows else 0, rows[1] if rows else 0, light_spp,
-                         progressive_frame)
+                         progressive_frame, 1 if lcg_seed is not None else 0, lcg_seed or 0)
         if accum is not None:
             assert accum.dtype == np.float32 and accum.shape == (info.res_y, info.res_x, 3) and accum.flags.c_contiguous
             out = accum
@@ -403,3 +407,8 @@ def rnd(seed, pixel, n, sphere, glibc_rand_max=False):
     return out, calls
 
 
+def crt_rand(seed, n):
+    """The first n draws of the MSVC CRT rand() after srand(seed) (the oracle's lcg mode)."""
+    out = (C.c_int32 * n)()
+    lib().orc_crt_rand(seed, n, out)
+    return list(out)

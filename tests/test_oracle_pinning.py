@@ -133,6 +133,15 @@ def test_rng_draw_order_identical_to_reference(oracle_mod, sphere):
     np.testing.assert_array_equal(bits(vals), bits(g[f"rnd{sphere}_vals"]))
 
 
+def test_crt_rand_mode_is_the_msvc_sequence(oracle_mod):
+    """The oracle's lcg mode (orc_options.lcg: the reference runs' own RNG) draws
+    the MSVC CRT sequence: after srand(1), rand() returns 41, 18467, 6334, 26500, 19169, ... (the
+    published first values of that generator), and 15-bit draws for any seed."""
+    assert oracle_mod.crt_rand(1, 8) == [41, 18467, 6334, 26500, 19169, 15724, 11478, 29358]
+    d = oracle_mod.crt_rand(12345, 1000)
+    assert min(d) >= 0 and max(d) <= 0x7FFF and len(set(d)) > 900
+
+
 def test_dragon_assignment1_traversal_count_matches_reference_run(oracle_mod, tmp_path):
     """the reference renders dragon_assignment1 (Whitted, BVH, 512x512) with
     1 436 437 BVH::Traverse calls (closest + shadow).  RNG-independent, so it pins primitive
