@@ -216,8 +216,8 @@ static PrimRecord pack_prim(const drt_prim& p, uint32_t mat, uint32_t obj) {
 // that every child's [lo, hi] is covered by [p + ql * s, p + qh * s] with 0 <= ql, qh <= 255 and
 // every such plane an exact float (|k| + 255 < 2^24).  False if no exponent fits (non-finite or
 // enormous coordinates): the scene then keeps the binary tree for its shadow queries.
-static bool quantize_axis(const double* lo, const double* hi, int n, float& p, uint32_t& ebits, uint32_t& qlo,
-                          uint32_t& qhi) {
+static bool quantize_axis(const double* lo, const double* hi, int n, float& p, uint32_t& ebits, uint32_t* qlo,
+                          uint32_t* qhi) {
   double nlo = lo[0], nhi = hi[0];
   for (int k = 1; k < n; k++) {
     nlo = std::min(nlo, lo[k]);
@@ -232,14 +232,14 @@ static bool quantize_axis(const double* lo, const double* hi, int n, float& p, u
     const double s = std::ldexp(1.0, E);
     const double k0 = std::floor(nlo / s);
     if (std::fabs(k0) + 256.0 >= 16777216.0) continue;
-    uint32_t L = 0, H = 0;
+    uint32_t L[kWideW] = {}, H[kWideW] = {};  // byte k & 3 of word k >> 2: child k
     bool ok = true;
     const float pf = (float)(k0 * s), sf = (float)s;
     if ((double)pf != k0 * s) continue;
     if (E > 50) return false;
-    for (int k = 0; k < 4 && ok; k++) {
+    for (int k = 0; k < kWideK && ok; k++) {
       if (k >= n) {  // unused slot: an inverted box (lo 255 > hi 0)
-        L |= 255u << (8 * k);
+        L[k >> 2] |= 255u << (8 * (k & 3));
         continue;
       }
       const double ql = std::floor(lo[k] / s) - k0, qh = std::ceil(hi[k] / s) - k0;
@@ -253,14 +253,16 @@ static bool quantize_axis(const double* lo, const double* hi, int n, float& p, u
         ok = false;
         break;
       }
-      L |= (uint32_t)ql << (8 * k);
-      H |= (uint32_t)qh << (8 * k);
+      L[k >> 2] |= (uint32_t)ql << (8 * (k & 3));
+      H[k >> 2] |= (uint32_t)qh << (8 * (k & 3));
     }
     if (!ok) continue;
     p = pf;
     ebits = (uint32_t)(E + 127);
-    qlo = L;
-    qhi = H;
+    for (int w = 0; w < kWideW; w++) {
+      qlo[w] = L[w];
+      qhi[w] = H[w];
+    }
     return true;
   }
   return false;
@@ -325,11 +327,11 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
     const Item it = st.back();
     st.pop_back();
     maxd = std::max(maxd, it.depth);
-    uint32_t ch[4];
+    uint32_t ch[kWideK];
     int n = 2;
     ch[0] = nodes[it.node].index;
     ch[1] = ch[0] + 1;
-    while (n < 4) {
+    while (n < kWideK) {
       int best = -1;
       double ba = -1.0;
       for (int k = 0; k < n; k++)
@@ -352,13 +354,13 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
     }
     WideNodeRecord r{};
     for (int a = 0; a < 3; a++) {
-      double lo[4], hi[4];
+      double lo[kWideK], hi[kWideK];
       for (int k = 0; k < n; k++) {
         lo[k] = nodes[ch[k]].bmin[a];
         hi[k] = nodes[ch[k]].bmax[a];
       }
       uint32_t e = 0;
-      if (!quantize_axis(lo, hi, n, r.p[a], e, r.q[2 * a], r.q[2 * a + 1])) return false;
+      if (!quantize_axis(lo, hi, n, r.p[a], e, r.q + kWideW * (2 * a), r.q + kWideW * (2 * a + 1))) return false;
       r.ebits |= e << (8 * a);
     }
     // children pushed in reverse so the first child's subtree follows its parent in memory
@@ -373,7 +375,7 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
     }
     out[it.slot] = r;
   }
-  if (3 * maxd > kWideMaxStack) return false;
+  if ((kWideK - 1) * maxd > kWideMaxStack) return false;  // a node pushes at most kWideK - 1 children
   root = 0;
   return true;
 }

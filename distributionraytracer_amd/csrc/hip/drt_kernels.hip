@@ -1228,8 +1228,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     first = bl.x;
     cnt = bl.y;
   }
+  // (a shadow-tree node record is 4 slots, 8 for the 8-ary tree of -DDRT_WIDE8)
   const float4* rec = leaf ? S.prims + 3 * (size_t)first
-                           : (verify ? S.wleaf + 2 * (size_t)cur : (wide ? S.wnodes : S.nodes) + 4 * (size_t)cur);
+                           : (verify ? S.wleaf + 2 * (size_t)cur
+                                     : (wide ? S.wnodes + (size_t)(kWideK == 8 ? 8 : 4) * cur : S.nodes + 4 * (size_t)cur));
   float4 s0, s1, s2, s3, s4, s5;
   bool uni_done = false;
   if (UNI && visit) {
@@ -1260,7 +1262,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     // headline; the closest-chain pass of in-order frames lost 1.5 % with it and keeps 1).
     if (LEAF1 != 2 || inner || whole) s3 = rec[3];
   }
-  if (leaf && whole && cnt > 1) {
+  if ((leaf && whole && cnt > 1) || (kWideK == 8 && WIDE && inner && wide)) {  // (8-ary node: its descriptors)
     s4 = rec[4];
     s5 = rec[5];
   }
@@ -1280,15 +1282,36 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     const uint32_t eb = __float_as_uint(s0.w);
     const float scx = __uint_as_float((eb & 0xffu) << 23), scy = __uint_as_float(((eb >> 8) & 0xffu) << 23),
                 scz = __uint_as_float(((eb >> 16) & 0xffu) << 23);
-    const uint32_t lx = __float_as_uint(s1.x), hx = __float_as_uint(s1.y), ly = __float_as_uint(s1.z),
-                   hy = __float_as_uint(s1.w), lz = __float_as_uint(s2.x), hz = __float_as_uint(s2.y);
     const bool px = L.q.sx(), py = L.q.sy(), pz = L.q.sz();
-    const uint32_t nx = px ? lx : hx, fx = px ? hx : lx, ny = py ? ly : hy, fy = py ? hy : ly, nz = pz ? lz : hz,
-                   fz = pz ? hz : lz;
-    const uint32_t d[4] = {__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w)};
-    float tn[4];
-    bool hk[4];
+    // per axis the near / far plane bytes of every child (byte k & 3 of word k >> 2 is child k)
+    uint32_t nx[kWideW], fx[kWideW], ny[kWideW], fy[kWideW], nz[kWideW], fz[kWideW];
+    uint32_t d[kWideK];
+    if constexpr (kWideK == 4) {
+      const uint32_t lx = __float_as_uint(s1.x), hx = __float_as_uint(s1.y), ly = __float_as_uint(s1.z),
+                     hy = __float_as_uint(s1.w), lz = __float_as_uint(s2.x), hz = __float_as_uint(s2.y);
+      nx[0] = px ? lx : hx; fx[0] = px ? hx : lx;
+      ny[0] = py ? ly : hy; fy[0] = py ? hy : ly;
+      nz[0] = pz ? lz : hz; fz[0] = pz ? hz : lz;
+      d[0] = __float_as_uint(s3.x); d[1] = __float_as_uint(s3.y); d[2] = __float_as_uint(s3.z); d[3] = __float_as_uint(s3.w);
+    } else {  // 8-ary record: s1 / s2 / s3 = (lo w0, lo w1, hi w0, hi w1) of x / y / z, s4 / s5 the descriptors
+      const float4 q3[3] = {s1, s2, s3};
+      const bool pp[3] = {px, py, pz};
+      uint32_t* nn[3] = {nx, ny, nz};
+      uint32_t* ff[3] = {fx, fy, fz};
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        const uint32_t l0 = __float_as_uint(q3[a].x), l1 = __float_as_uint(q3[a].y), h0 = __float_as_uint(q3[a].z),
+                       h1 = __float_as_uint(q3[a].w);
+        nn[a][0] = pp[a] ? l0 : h0; nn[a][1] = pp[a] ? l1 : h1;
+        ff[a][0] = pp[a] ? h0 : l0; ff[a][1] = pp[a] ? h1 : l1;
+      }
+      d[0] = __float_as_uint(s4.x); d[1] = __float_as_uint(s4.y); d[2] = __float_as_uint(s4.z); d[3] = __float_as_uint(s4.w);
+      d[4] = __float_as_uint(s5.x); d[5] = __float_as_uint(s5.y); d[6] = __float_as_uint(s5.z); d[7] = __float_as_uint(s5.w);
+    }
+    float tn[kWideK];
+    bool hk[kWideK];
 #ifdef DRT_WIDE_PK
+    static_assert(kWideK == 4, "packed decode: 4-ary records");
     // two children per packed-f32 instruction (v_pk_fma / v_pk_add / v_pk_mul): the same roundings
     typedef float f2v __attribute__((ext_vector_type(2)));
     const f2v ox2 = {L.q.o.x, L.q.o.x}, oy2 = {L.q.o.y, L.q.o.y}, oz2 = {L.q.o.z, L.q.o.z};
@@ -1299,12 +1322,12 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     for (int h = 0; h < 2; h++) {
       const int a = 16 * h, b = 16 * h + 8;
       auto dq = [&](uint32_t w) { return f2v{(float)((w >> a) & 0xffu), (float)((w >> b) & 0xffu)}; };
-      const f2v tnx = (__builtin_elementwise_fma(dq(nx), sx2, px2) - ox2) * ix2;
-      const f2v tfx = (__builtin_elementwise_fma(dq(fx), sx2, px2) - ox2) * ix2;
-      const f2v tny = (__builtin_elementwise_fma(dq(ny), sy2, py2) - oy2) * iy2;
-      const f2v tfy = (__builtin_elementwise_fma(dq(fy), sy2, py2) - oy2) * iy2;
-      const f2v tnz = (__builtin_elementwise_fma(dq(nz), sz2, pz2) - oz2) * iz2;
-      const f2v tfz = (__builtin_elementwise_fma(dq(fz), sz2, pz2) - oz2) * iz2;
+      const f2v tnx = (__builtin_elementwise_fma(dq(nx[0]), sx2, px2) - ox2) * ix2;
+      const f2v tfx = (__builtin_elementwise_fma(dq(fx[0]), sx2, px2) - ox2) * ix2;
+      const f2v tny = (__builtin_elementwise_fma(dq(ny[0]), sy2, py2) - oy2) * iy2;
+      const f2v tfy = (__builtin_elementwise_fma(dq(fy[0]), sy2, py2) - oy2) * iy2;
+      const f2v tnz = (__builtin_elementwise_fma(dq(nz[0]), sz2, pz2) - oz2) * iz2;
+      const f2v tfz = (__builtin_elementwise_fma(dq(fz[0]), sz2, pz2) - oz2) * iz2;
 #pragma unroll
       for (int j = 0; j < 2; j++) {
         const float t0 = fmaxf(fmaxf(tnx[j], tny[j]), tnz[j]), t1 = fminf(fminf(tfx[j], tfy[j]), tfz[j]);
@@ -1331,28 +1354,28 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
                           __builtin_fmaf(255.0f, fabsf(Sz), fabsf(Bz)));
     const float D2 = __builtin_fmaf(M, 0x1p-20f, 0x1p-99f);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int sh = 8 * k;
-      const float tnx = __builtin_fmaf((float)((nx >> sh) & 0xffu), Sx, Bx);
-      const float tfx = __builtin_fmaf((float)((fx >> sh) & 0xffu), Sx, Bx);
-      const float tny = __builtin_fmaf((float)((ny >> sh) & 0xffu), Sy, By);
-      const float tfy = __builtin_fmaf((float)((fy >> sh) & 0xffu), Sy, By);
-      const float tnz = __builtin_fmaf((float)((nz >> sh) & 0xffu), Sz, Bz);
-      const float tfz = __builtin_fmaf((float)((fz >> sh) & 0xffu), Sz, Bz);
+    for (int k = 0; k < kWideK; k++) {
+      const int w = k >> 2, sh = 8 * (k & 3);
+      const float tnx = __builtin_fmaf((float)((nx[w] >> sh) & 0xffu), Sx, Bx);
+      const float tfx = __builtin_fmaf((float)((fx[w] >> sh) & 0xffu), Sx, Bx);
+      const float tny = __builtin_fmaf((float)((ny[w] >> sh) & 0xffu), Sy, By);
+      const float tfy = __builtin_fmaf((float)((fy[w] >> sh) & 0xffu), Sy, By);
+      const float tnz = __builtin_fmaf((float)((nz[w] >> sh) & 0xffu), Sz, Bz);
+      const float tfz = __builtin_fmaf((float)((fz[w] >> sh) & 0xffu), Sz, Bz);
       const float t0 = fmaxf(fmaxf(tnx, tny), tnz), t1 = fminf(fminf(tfx, tfy), tfz);
       hk[k] = fmaxf(t0, 0.0f) < t1 + D2;
       tn[k] = t0;
     }
 #else  // the reference arithmetic on the decoded planes
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int sh = 8 * k;
-      const float tnx = (__builtin_fmaf((float)((nx >> sh) & 0xffu), scx, s0.x) - L.q.o.x) * L.q.ix;
-      const float tfx = (__builtin_fmaf((float)((fx >> sh) & 0xffu), scx, s0.x) - L.q.o.x) * L.q.ix;
-      const float tny = (__builtin_fmaf((float)((ny >> sh) & 0xffu), scy, s0.y) - L.q.o.y) * L.q.iy;
-      const float tfy = (__builtin_fmaf((float)((fy >> sh) & 0xffu), scy, s0.y) - L.q.o.y) * L.q.iy;
-      const float tnz = (__builtin_fmaf((float)((nz >> sh) & 0xffu), scz, s0.z) - L.q.o.z) * L.q.iz;
-      const float tfz = (__builtin_fmaf((float)((fz >> sh) & 0xffu), scz, s0.z) - L.q.o.z) * L.q.iz;
+    for (int k = 0; k < kWideK; k++) {
+      const int w = k >> 2, sh = 8 * (k & 3);
+      const float tnx = (__builtin_fmaf((float)((nx[w] >> sh) & 0xffu), scx, s0.x) - L.q.o.x) * L.q.ix;
+      const float tfx = (__builtin_fmaf((float)((fx[w] >> sh) & 0xffu), scx, s0.x) - L.q.o.x) * L.q.ix;
+      const float tny = (__builtin_fmaf((float)((ny[w] >> sh) & 0xffu), scy, s0.y) - L.q.o.y) * L.q.iy;
+      const float tfy = (__builtin_fmaf((float)((fy[w] >> sh) & 0xffu), scy, s0.y) - L.q.o.y) * L.q.iy;
+      const float tnz = (__builtin_fmaf((float)((nz[w] >> sh) & 0xffu), scz, s0.z) - L.q.o.z) * L.q.iz;
+      const float tfz = (__builtin_fmaf((float)((fz[w] >> sh) & 0xffu), scz, s0.z) - L.q.o.z) * L.q.iz;
       const float t0 = fmaxf(fmaxf(tnx, tny), tnz), t1 = fminf(fminf(tfx, tfy), tfz);
       hk[k] = fmaxf(t0, 0.0f) < t1;  // t0 < t1 && t1 > 0
       tn[k] = t0;
@@ -1364,7 +1387,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     int ci = -1;
     float best = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < kWideK; k++) {
 #ifdef DRT_WIDE_NEAREST  // (A/B) the hit child entered first
       const bool take = hk[k] && (ci < 0 || tn[k] < best);
 #else
@@ -1381,7 +1404,7 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
     // order; 1 947 with ascending slots pushed in slot order, 1 951-1 953 descending and reversed
     // (profiles/r04_wide_order_push_ab.jsonl).
 #pragma unroll
-    for (int k = 3; k >= 0; k--) {
+    for (int k = kWideK - 1; k >= 0; k--) {
       if (hk[k] && k != ci) {
         if (spa < kWideLds) *(LdsU32*)(lds + spa) = d[k];
         else ov_desc[(spa - kWideLds) >> kRowShift] = d[k];
@@ -1393,7 +1416,10 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       }
     }
     L.spa = spa;
-    L.cur = ci == 0 ? d[0] : (ci == 1 ? d[1] : (ci == 2 ? d[2] : d[3]));
+    uint32_t nxt = d[0];
+#pragma unroll
+    for (int k = 1; k < kWideK; k++) nxt = ci == k ? d[k] : nxt;
+    L.cur = nxt;
     fl |= ci < 0 ? LF_POP : 0u;
   }
   if (WIDE && verify) {  // the exact reference leaf box of primitive `cur`, hit within range

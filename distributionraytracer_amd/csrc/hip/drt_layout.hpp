@@ -70,20 +70,42 @@ struct NodeRecord {
   float box[12];
   uint32_t desc[4];
 };
-struct WideNodeRecord {
+// Children per shadow-tree node: 4 (64-B records), or 8 with -DDRT_WIDE8 (A/B, round 6): a 128-B record —
+//   s0 = (p, ebits), s1 = lo.x[8], hi.x[8] (two words each), s2 = y, s3 = z, s4 / s5 = desc[0..3] / [4..7],
+//   s6, s7 unused — one 128-B line per visit, six slot loads, half the tree levels.
+#ifdef DRT_WIDE8
+constexpr int kWideK = 8;
+#else
+constexpr int kWideK = 4;
+#endif
+constexpr int kWideW = kWideK / 4;  // words per plane (one byte per child)
+struct WideNodeRecord4 {
   float p[3];
   uint32_t ebits;
   uint32_t q[6];  // lo.x, hi.x, lo.y, hi.y, lo.z, hi.z (byte k = child k)
   uint32_t pad[2];
   uint32_t desc[4];
 };
+struct WideNodeRecord8 {
+  float p[3];
+  uint32_t ebits;
+  uint32_t q[12];  // per plane (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) two words: byte k & 3 of word k >> 2
+  uint32_t desc[8];
+  uint32_t pad[8];
+};
+#ifdef DRT_WIDE8
+#define WideNodeRecord WideNodeRecord8
+#else
+#define WideNodeRecord WideNodeRecord4
+#endif
 struct LeafBoxRecord {
   float box[6];
   uint32_t pad[2];
 };
 static_assert(sizeof(PrimRecord) == 48, "prim record is 48 B");
 static_assert(sizeof(NodeRecord) == 64, "node record is 64 B");
-static_assert(sizeof(WideNodeRecord) == 64, "wide node record is 64 B");
+static_assert(sizeof(WideNodeRecord4) == 64, "4-ary wide node record is 64 B");
+static_assert(sizeof(WideNodeRecord8) == 128, "8-ary wide node record is 128 B");
 static_assert(sizeof(LeafBoxRecord) == 32, "leaf box record is 32 B");
 
 inline float bits_as_float(uint32_t u) {

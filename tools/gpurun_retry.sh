@@ -6,7 +6,7 @@ for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout $to -- "$cmd" > $log 2>&1
   rc=$?
   [ $rc -ne 3 ] && exit $rc
-  grep -q "slot(s) on this pod are busy\|no box" $log || exit $rc
+  grep -q "slot(s) on this pod are busy\|no free box\|no box" $log || exit $rc
   sleep 120
 done
 exit 3
