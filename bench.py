@@ -391,6 +391,12 @@ def main():
         pass1_ms, pass2_ms = r.frame_pass_times(serial)
     except AttributeError:  # an A/B build (DRT_LIBRARY) older than drt_frame_pass_times
         pass1_ms, pass2_ms = [], []
+    stage_ms = None  # the last serial frame's pass-2 launches (wf_gen, stream, wf_combine), HIP events
+    if wavefront:
+        try:
+            stage_ms = r.frame_stage_times()
+        except (AttributeError, RuntimeError):  # (an A/B build older than drt_frame_stage_times)
+            stage_ms = None
     frame_check = None
     if args.check_frame:
         step(shard_p)  # assemble one more frame, then compare it with a one-shot whole frame
@@ -473,6 +479,31 @@ def main():
             if name == "replay":
                 row["kernels"] = ("wf_gen + trace_stream<shadow> + wf_combine" if wavefront else
                                   f"path_persistent<{args.accel.upper()}> replay")
+                if stage_ms:
+                    # each launch of the wavefront pass 2 on its own: its device time in
+                    # the last serial frame, and the bytes it streams — wf_gen writes every (level, pair)
+                    # query record (32 B) and its Phong factors (8 B) plus a 16-B record per level; the
+                    # stream moves the pass's algorithmic shadow-tree bytes; wf_combine reads the answers
+                    # (1 B), factors and level records and writes the frame (12 B per pixel)
+                    levels = args.max_depth + 1
+                    n_quad = 1 if args.scene == "synthetic" else 2
+                    pairs = n_quad * max(1, args.light_spp) + 1
+                    slots = plan["sample_slots"]
+                    gen_b = slots * levels * (pairs * 40 + 16)
+                    comb_b = slots * levels * (pairs * 9 + 16) + 12 * slots // max(1, args.spp)
+                    la = {}
+                    for key, label, bb in (("wf_gen", "wf_gen", gen_b), ("stream", "trace_stream" if args.accel == "bvh"
+                                            else "path_persistent<GRID> query stream", b),
+                                           ("wf_combine", "wf_combine (reduce folded in)", comb_b)):
+                        lm = float(stage_ms[key])
+                        e = {"kernel": label, "ms": round(lm, 3), "bytes": int(bb),
+                             "achieved": round(bb / max(1e-9, lm * 1e-3) / 1e9, 1)}
+                        if key == "stream" and ceiling:
+                            e["frac"] = round(e["achieved"] / ceiling["peak_GB_per_s"], 4)
+                        elif key != "stream":
+                            e["hbm_frac"] = round(e["achieved"] / HBM_PEAK_GBS, 4)
+                        la[key] = e
+                    row["launches"] = la
             if ceiling:
                 row["frac"] = round(row["achieved"] / ceiling["peak_GB_per_s"], 4)
             if pp and pp.get("read_bytes") is not None:

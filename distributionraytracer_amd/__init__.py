@@ -348,6 +348,14 @@ class Renderer:
             check(n, self.h, "drt_frame_pass_times")
         return np.array(a[:n]), np.array(b[:n])
 
+    def frame_stage_times(self):
+        """{wf_gen, stream, wf_combine} ms of the last wavefront frame's pass-2 launches (drt_frame_stage_times)."""
+        out = (C.c_double * 3)()
+        n = _lib.load().drt_frame_stage_times(self.h, out)
+        if n < 0:
+            check(n, self.h, "drt_frame_stage_times")
+        return {"wf_gen": out[0], "stream": out[1], "wf_combine": out[2], "chunks": n}
+
     def wave_times(self, pass_index=0, max_waves=1 << 14):
         """Per resident wave of the last stats frame's persistent launch (pass 0 or 1): (start, end)
         s_memrealtime stamps in us (100 MHz clock), rows of waves that ran; (drt_frame_wave_times)."""

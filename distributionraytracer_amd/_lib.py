@@ -125,6 +125,7 @@ SIGNATURES = {
                                   C.POINTER(C.c_double)]),
     "drt_frame_pass_times": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "drt_frame_wave_times": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_uint64), C.c_int64]),
+    "drt_frame_stage_times": (C.c_int, [_vp, C.POINTER(C.c_double)]),
     "drt_frame_resolution": (C.c_int, [_vp, _i32]),
     "drt_group_create": (C.c_int, [C.POINTER(_vp), C.c_int, _i32]),
     "drt_group_destroy": (None, [_vp]),

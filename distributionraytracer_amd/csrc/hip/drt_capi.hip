@@ -105,6 +105,12 @@ struct drt_ctx {
   // s_memrealtime stamps (drt_frame_wave_times); wave_slots = waves per pass
   DevBuf d_wave_times;
   uint32_t wave_slots = 0;
+  // the last wavefront frame's launches: per chunk (<= kStageChunks) the events after its wf_gen, its
+  // shadow-query stream and its wf_combine (drt_frame_stage_times); stage_chunks = chunks recorded
+  static constexpr int kStageChunks = 64;
+  std::vector<hipEvent_t> stage_ev;
+  int stage_chunks = 0;
+  int stage_frame_ev = -1;  // ring slot of that frame (its end-of-pass-1 event opens chunk 0)
   uint32_t wroot = 0, n_wide = 0;
   // grid
   bool has_grid = false;
@@ -433,6 +439,8 @@ void drt_destroy(drt_ctx* c) {
   for (auto& e : c->ring)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->tev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->stage_ev)
     if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < DRT_FRAME_SLOTS; k++) {
     if (c->aux[k]) {
@@ -1388,6 +1396,14 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     F2.part_items = (uint32_t)((F2.n_items + 7) / 8);
     F2.work_counter = d_counter.as<unsigned int>() + 256;
     if (F2.wave_times) F2.wave_times += 2u * c->wave_slots;  // pass 2's launches (persistent replay / MODE_QSTREAM)
+    if (wavefront) {  // drt_frame_stage_times: this frame's launches
+      if (c->stage_ev.empty()) {
+        c->stage_ev.assign(3 * drt_ctx::kStageChunks, nullptr);
+        for (auto& e : c->stage_ev) DRT_HIP(c, hipEventCreate(&e));
+      }
+      c->stage_chunks = 0;
+      c->stage_frame_ev = (int)(drt_ctx::kEv * ((c->frames - 1) % drt_ctx::kRing));
+    }
     for (uint32_t k = 0; wavefront && k < P.wf_chunks; k++) {
       W.slot0 = (uint32_t)(k * P.wf_chunk);
       W.n_slots = (uint32_t)std::min<uint64_t>(P.wf_chunk, P.n_slots - W.slot0);
@@ -1398,6 +1414,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       W.band = (W.n_slots + (uint32_t)W.bands - 1u) / (uint32_t)W.bands;
       launch_wf_gen(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
+      const bool stage = k < (uint32_t)drt_ctx::kStageChunks && !c->stage_ev.empty();
+      if (stage) DRT_HIP(c, hipEventRecord(c->stage_ev[3 * k], st));
       const uint64_t q = (uint64_t)W.levels * (uint64_t)W.pairs * W.band * (uint64_t)W.bands;
       const uint32_t part_len = (uint32_t)((uint64_t)W.levels * W.pairs * W.band);
       unsigned int* counter = d_counter.as<unsigned int>() + 256u * (1u + k);
@@ -1438,9 +1456,12 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);
         DRT_HIP(c, hipGetLastError());
       }
+      if (stage) DRT_HIP(c, hipEventRecord(c->stage_ev[3 * k + 1], st));
       if (P.wf_fold) launch_wf_combine_reduce(S, F2, W, P.R, st);
       else launch_wf_combine(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
+      if (stage) DRT_HIP(c, hipEventRecord(c->stage_ev[3 * k + 2], st));
+      if (stage) c->stage_chunks = (int)k + 1;
     }
     folded = wavefront && P.wf_fold;
     if (!wavefront) launch_path_persistent(S, F2, c->accel, c->tri_only, stats, st);
@@ -1574,6 +1595,25 @@ int drt_frame_pass_times(drt_ctx* c, int max_frames, double* pass1_ms, double* p
     if (pass2_ms) pass2_ms[i] = b;
   }
   return n;
+}
+
+int drt_frame_stage_times(drt_ctx* c, double out_ms[3]) {
+  if (!c || !out_ms) return DRT_E_INVALID;
+  if (c->stage_chunks <= 0 || c->stage_frame_ev < 0) DRT_FAIL(c, DRT_E_STATE, "no wavefront frame recorded");
+  DRT_HIP(c, hipSetDevice(c->device));
+  out_ms[0] = out_ms[1] = out_ms[2] = 0.0;
+  hipEvent_t prev = c->ring[c->stage_frame_ev + 3];  // end of pass 1
+  for (int k = 0; k < c->stage_chunks; k++) {
+    hipEvent_t* e = &c->stage_ev[3 * k];
+    DRT_HIP(c, hipEventSynchronize(e[2]));
+    float a = 0, b = 0, d = 0;
+    DRT_HIP(c, hipEventElapsedTime(&a, prev, e[0]));
+    DRT_HIP(c, hipEventElapsedTime(&b, e[0], e[1]));
+    DRT_HIP(c, hipEventElapsedTime(&d, e[1], e[2]));
+    out_ms[0] += a; out_ms[1] += b; out_ms[2] += d;
+    prev = e[2];
+  }
+  return c->stage_chunks;
 }
 
 int drt_frame_wave_times(drt_ctx* c, int pass, uint64_t* start_end, int64_t max_waves) {

@@ -300,6 +300,13 @@ int drt_frame_spans(drt_ctx* ctx, int max_frames, double* path_start, double* pa
  * wave.  Returns the number of wave slots written (<= max_waves).  No reference counterpart: it measures
  * the tail of a launch. */
 int drt_frame_wave_times(drt_ctx* ctx, int pass, uint64_t* start_end, int64_t max_waves);
+
+/* Device time of each launch of the last wavefront frame's pass 2 (the frame issued last whose plan
+ * has `wavefront`): out_ms = {wf_gen, shadow-query stream (trace_stream / the Grid's MODE_QSTREAM),
+ * wf_combine}, summed over its chunks (HIP events between the launches on the frame's stream; the first
+ * 64 chunks).  Waits for that frame.  Returns the chunks counted; DRT_E_STATE before any wavefront
+ * frame.  Read it before the next frame is issued. */
+int drt_frame_stage_times(drt_ctx* ctx, double out_ms[3]);
 /* The same frames' passes: a two-pass frame (drt_frame_plan.passes == 2) is the closest-chain pass
  * then the replay pass, timed from the path-kernel start to the end of the first launch and from
  * there to the path-kernel end (HIP events on the frame's stream; pass1 + pass2 = path_ms of

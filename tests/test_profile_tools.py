@@ -22,6 +22,8 @@ GEN = "drt::wf_gen_kernel(drt::SceneArgs, drt::FrameArgs, drt::WfArgs)"
 TRACE = "void drt::trace_stream<true, 2, 7, false>(drt::SceneArgs, drt::TraceArgs)"
 TRACE_ST = "void drt::trace_stream<true, 2, 7, true>(drt::SceneArgs, drt::TraceArgs)"
 COMB = "drt::wf_combine_kernel(drt::SceneArgs, drt::FrameArgs, drt::WfArgs)"
+# round 6: the combine with the frame's reduce folded in (the default)
+COMBR = "drt::wf_combine_reduce_kernel(drt::SceneArgs, drt::FrameArgs, drt::WfArgs, drt::ReduceArgs, unsigned int)"
 QSTREAM = "void drt::path_persistent<true, false, 11, 5, 1>(drt::SceneArgs, drt::FrameArgs)"
 GCHAIN = "void drt::path_persistent<true, false, 7, 5, 1>(drt::SceneArgs, drt::FrameArgs)"
 REDUCE = "drt::reduce_kernel(drt::ReduceArgs)"
@@ -100,3 +102,16 @@ def test_pmc_traffic_last_frame_sums_the_second_pass(tmp_path):
     fr = pmc_traffic.last_frame(c)
     assert [k[0] for k in fr] == [9, 10, 11, 12]          # the last non-stats frame, all four dispatches
     assert pmc_traffic._sum(c, fr[1:])["WRITE_SIZE"] == 10 + 11 + 12
+
+
+def test_rocprof_union_counts_the_folded_combine(tmp_path):
+    """Round 6: a wavefront frame ends with wf_combine_reduce_kernel (no reduce launch); it is part of the frame."""
+    d = []
+    for k in range(2):  # 1 warmup + 1 timed
+        d += [x for x in frame(CHAIN, [GEN, TRACE, COMBR], 0, 100_000_000 * (k + 1)) if x[0] != REDUCE]
+    write_trace(tmp_path / "t", d)
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "rocprof_union.py"), str(tmp_path / "t"), "--steps", "1",
+                          "--warmup", "1", "--settle", "0"], capture_output=True, text=True, check=True).stdout
+    r = json.loads(out)
+    assert r["dispatches_per_frame"] == 4
+    assert abs(r["kernel_ms_per_step_union"] - 20.0) < 0.01 and COMBR in r["kernels"]
