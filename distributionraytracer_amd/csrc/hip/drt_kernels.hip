@@ -2043,6 +2043,88 @@ __device__ bool wf_level(const SceneArgs& S, const FrameArgs& F, const WfArgs& W
   wf_st(&W.lvl[li_], make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24))));
   return more;
 }
+#ifdef DRT_WF_FULLWAVE
+// (A/B, round 6) wf_level with every query store made by the whole wave: a lane whose chain has ended
+// (`live` false) or missed at this level stores the empty-slot marker (thr = -1) in the same store
+// instruction as the lanes that store queries, so that each 128-B line of the query arrays is written
+// whole by one instruction instead of in pieces by the level's stores and wf_mark_empty's; its
+// direction and Phong factors are don't-care values.  The same queries, factors and level records.
+__device__ bool wf_level_fw(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, uint32_t slot, int l,
+                            const RayP& q, bool live, bool hit, float t, uint32_t prim, V3& ls, uint32_t pmix,
+                            uint32_t& rk, RayP& next) {
+  const size_t li_ = (size_t)l * W.n_slots + slot;
+  if (live && !hit) {  // main.cpp:351-357
+    const V3 c = cclamp(background(S, q.d));
+    wf_st(&W.lvl[li_], make_float4(c.x, c.y, c.z, __uint_as_float(WF_MISS << 24)));
+  }
+  V3 hitP = mk(0, 0, 0), N = mk(0, 0, 1), V = mk(0, 0, 1);
+  bool outside = true;
+  uint32_t mat = 0;
+  if (hit) {
+    hitP = add(q.o, mul(q.d, t));
+    N = normalize(prim_normal(S.prims, prim, q, t));
+    outside = dot(q.d, N) < 0.0f;
+    if (!outside) N = neg(N);
+    mat = prim_material(S.prims[3 * prim]);
+    V = neg(normalize(q.d));
+  }
+  V3 lightPos = mk(0, 0, 0);
+  for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // setup_shadow for every pair the light loop visits
+    if (!wf_pair_used(S, F, j)) continue;
+    const size_t qi = wf_q(W, l, u++, slot);
+    float4 ra = make_float4(0.f, 0.f, 0.f, -1.0f), rb = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 nlv = make_float2(0.f, 0.f);
+    if (hit) {
+      const int li = light_of_pair(j, F);
+      lightPos = light_point(S.lights[li], ls, j - li * F.light_spp, F);
+      V3 Lv = sub(lightPos, hitP);
+      const V3 Ls = Lv;
+      Lv = normalize(Lv);
+      const V3 H = normalize(add(Lv, V));
+      const float NdotL = smax(dot(N, Lv), 0.0f), NdotH = smax(dot(N, H), 0.0f);
+      const V3 so = add(hitP, mul(N, 1e-4f));
+      const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
+      ra = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
+      rb = make_float4(sd.x, sd.y, sd.z, 0.0f);
+      nlv = make_float2(NdotL, NdotH);
+    }
+    wf_st(&W.rays[qi], ra);
+    wf_st(&W.rays_b[qi], rb);
+    wf_st(&W.nl[qi], nlv);
+  }
+  if (!hit) return false;
+  uint32_t flags = 0u;
+  bool more = false;
+  if (l + 1 > F.max_depth) {  // depth > MAX_DEPTH: the accumulated colour, unclamped (main.cpp:454)
+    flags = WF_DEEP;
+  } else {
+    const drt_material m = S.mats[mat];
+    float kr = m.refl;
+    float ior2 = m.ior;
+    if (!outside) ior2 = 1.0f;
+    const float eta = 1.0f / ior2;
+    const V3 Vt = sub(mul(N, dot(V, N)), V);
+    const float sin_t = eta * length(Vt);
+    if (m.trans > 0.0f && sin_t >= 1.0f) kr = 1.0f;
+    if (m.ks > 0.0f) {
+      V3 R = sub(mul(mul(N, dot(V, N)), 2.0f), V);
+      if (W.inorder) {
+        KRng rng{F.seed, pmix, rk};
+        R = normalize(add(R, mul(rnd_unit_sphere(rng), F.roughness)));
+        rk = rng.k;
+      } else {
+        R = normalize(R);
+      }
+      flags = WF_REFL | (dot(R, N) > 0.0f ? WF_RN : 0u) | (kr == 1.0f && m.refl != 1.0f ? WF_KR1 : 0u);
+      next = make_ray(add(hitP, mul(N, 1e-4f)), R);
+      ls = lightPos;
+      more = true;
+    }
+  }
+  wf_st(&W.lvl[li_], make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24))));
+  return more;
+}
+#endif
 // No shadow query at levels from..max_depth of chunk slot `slot` (past its chain's end; a miss level
 // has none either).
 __device__ __forceinline__ void wf_mark_empty(const WfArgs& W, int from, uint32_t slot) {
@@ -2678,6 +2760,28 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
                            ((float)(sb / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
                       : mk(0.5f, 0.5f, 0.0f);
     }
+#ifdef DRT_WF_FULLWAVE
+    bool live = true;
+    for (int lv = 0; lv <= md; lv++) {  // every level, every lane: the query stores are whole-wave
+      uint2 h = make_uint2(0u, 0xFFFFFFFFu);
+      if (live) h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)lv];
+      const bool hit = live && h.y != 0xFFFFFFFFu;
+      RayP next;
+      const bool more = wf_level_fw(S, F, W, slot, lv, q, live, hit, __uint_as_float(h.x), h.y, ls, pmix, rk, next);
+      live = more;
+      if (more) q = next;
+    }
+    l = W.levels;
+  } else {
+    RayP q0{};
+    V3 ls0 = mk(0, 0, 0);
+    uint32_t rk0 = 0;
+    for (int lv = 0; lv <= md; lv++) {
+      RayP next;
+      (void)wf_level_fw(S, F, W, slot, lv, q0, false, false, 0.0f, 0u, ls0, 0u, rk0, next);
+    }
+    l = W.levels;
+#else
     while (l <= md) {
       const uint2 h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)l];
       const bool hit = h.y != 0xFFFFFFFFu;
@@ -2687,6 +2791,7 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
       if (!more) break;
       q = next;
     }
+#endif
   }
   wf_mark_empty(W, l, slot);
 }
