@@ -2043,8 +2043,10 @@ __device__ bool wf_level(const SceneArgs& S, const FrameArgs& F, const WfArgs& W
   wf_st(&W.lvl[li_], make_float4(0.f, 0.f, 0.f, __uint_as_float(mat | (flags << 24))));
   return more;
 }
-#ifdef DRT_WF_FULLWAVE
-// (A/B, round 6) wf_level with every query store made by the whole wave: a lane whose chain has ended
+#ifndef DRT_WF_PIECEWISE
+// wf_level with every query store made by the whole wave (round 6; -DDRT_WF_PIECEWISE keeps the round-5
+// wf_level + wf_mark_empty: wf_gen 3.09 against 2.57 ms, headline -0.9 %, C3 -1.9 %, C4 -2.5 %,
+// profiles/r06_ab_wf_gen_fullwave.jsonl): a lane whose chain has ended
 // (`live` false) or missed at this level stores the empty-slot marker (thr = -1) in the same store
 // instruction as the lanes that store queries, so that each 128-B line of the query arrays is written
 // whole by one instruction instead of in pieces by the level's stores and wf_mark_empty's; its
@@ -2760,7 +2762,7 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
                            ((float)(sb / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
                       : mk(0.5f, 0.5f, 0.0f);
     }
-#ifdef DRT_WF_FULLWAVE
+#ifndef DRT_WF_PIECEWISE
     bool live = true;
     for (int lv = 0; lv <= md; lv++) {  // every level, every lane: the query stores are whole-wave
       uint2 h = make_uint2(0u, 0xFFFFFFFFu);
