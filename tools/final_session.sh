@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-end evidence at the head, in two GPU calls (outputs in gpurun_out/):
+#   X: parity tests, smoke, the gather ceilings (tools/ceiling.py) and the PMC records of the headline, C3 and
+#      Grid configs (tools/pmc_configs.sh)
+#   Y: the PMC records of C4 and C2, every BASELINE config (tools/configs.sh, 10 steps, CPU baselines), the
+#      bench line and a rocprofv3 --kernel-trace --stats run of the same command (tools/gpu_check.sh, no tests)
+#   usage: bash tools/final_session.sh X|Y
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out; mkdir -p $OUT
+case "${1:-X}" in
+  X)
+    bash tools/session.sh tests smoke || exit $?
+    timeout -k 10 300 python tools/ceiling.py $OUT/gather_ceiling.json || exit $?
+    PMC_ONLY="headline c3 grid" PMC_DB=$OUT/pmc_traffic.json bash tools/pmc_configs.sh || exit $?
+    ;;
+  Y)
+    PMC_ONLY="c4 c2" PMC_DB=$OUT/pmc_traffic.json bash tools/pmc_configs.sh || exit $?
+    CFG_STEPS=10 bash tools/configs.sh || exit $?
+    timeout -k 10 600 python bench.py --steps 20 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+    cut -c1-300 $OUT/bench.json
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
+        python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || exit $?
+    python tools/rocprof_union.py $OUT/prof --steps 20 --warmup 2 --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
+    cat $OUT/rocprof_union.json
+    ;;
+esac
