@@ -481,15 +481,19 @@ def main():
                                   f"path_persistent<{args.accel.upper()}> replay")
                 if stage_ms:
                     # each launch of the wavefront pass 2 on its own: its device time in
-                    # the last serial frame, and the bytes it streams — wf_gen writes every (level, pair)
-                    # query record (32 B) and its Phong factors (8 B) plus a 16-B record per level; the
+                    # the last serial frame, and the bytes it streams — wf_gen writes the query records (32 B;
+                    # BVH: real queries only, packed per 64-slot group) and every (level, pair)'s Phong factors
+                    # (8 B) plus a 16-B record per level; the
                     # stream moves the pass's algorithmic shadow-tree bytes; wf_combine reads the answers
                     # (1 B), factors and level records and writes the frame (12 B per pixel)
                     levels = args.max_depth + 1
                     n_quad = 1 if args.scene == "synthetic" else 2
                     pairs = n_quad * max(1, args.light_spp) + 1
                     slots = plan["sample_slots"]
-                    gen_b = slots * levels * (pairs * 40 + 16)
+                    if args.accel == "bvh":  # compact queries: records of the real queries only (WfArgs::compact)
+                        gen_b = mine["shadow_rays"] * 32 + slots * levels * (pairs * 8 + 16)
+                    else:  # the Grid's query stream reads the marker layout: every (level, pair) slot
+                        gen_b = slots * levels * (pairs * 40 + 16)
                     comb_b = slots * levels * (pairs * 9 + 16) + 12 * slots // max(1, args.spp)
                     la = {}
                     for key, label, bb in (("wf_gen", "wf_gen", gen_b), ("stream", "trace_stream" if args.accel == "bvh"

@@ -132,6 +132,7 @@ struct drt_ctx {
   DevBuf d_heads_s[DRT_FRAME_SLOTS];  // replay passes: frame heads, max_depth + 1 per resident lane
   // wavefront replay (WfArgs): shadow queries, their Phong factors and answers, per-level records
   DevBuf d_wf_rays_s[DRT_FRAME_SLOTS], d_wf_nl_s[DRT_FRAME_SLOTS], d_wf_occ_s[DRT_FRAME_SLOTS], d_wf_lvl_s[DRT_FRAME_SLOTS];
+  DevBuf d_wf_cnt_s[DRT_FRAME_SLOTS];  // compact queries: per (band, level, 64-slot group) the group's query count
   int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
@@ -947,6 +948,18 @@ struct Plan {
 };
 
 static void note_last_path_ms(drt_ctx* c);
+// Query slots a chunk's buffers hold beyond its sample slots: each of <= 8 bands rounded up to 256 slots.
+constexpr uint64_t kWfPad = 8u * 256u;
+// BVH wavefront frames pack each 64-slot group's queries (WfArgs::compact, round 6); DRT_WAVEFRONT_COMPACT=0
+// keeps the thr = -1 markers.  The Grid's query stream (MODE_QSTREAM) reads the marker layout.
+static bool wf_compact(const drt_ctx* c) {
+#ifdef DRT_WF_PIECEWISE
+  (void)c;
+  return false;
+#else
+  return c->accel == DRT_ACCEL_BVH && env_int("DRT_WAVEFRONT_COMPACT", 1) != 0;
+#endif
+}
 // Shadow-query slots per level of a wavefront replay: the (light, k) pairs the light loop visits — every
 // k of a quad light, k = 0 of a point light (next_light_pair).
 static uint64_t wf_pairs(const drt_ctx* c, int light_spp) {
@@ -1146,7 +1159,7 @@ static int plan_frame(drt_ctx* c, const drt_frame_params* p, Plan& P) {
     const uint64_t px = (uint64_t)std::max(1, slots);
     if (chunk > px) chunk -= chunk % px;
     chunk = std::max<uint64_t>(1, chunk);
-    const uint64_t q = ((uint64_t)md + 1u) * pairs * (chunk + 8u);
+    const uint64_t q = ((uint64_t)md + 1u) * pairs * (chunk + kWfPad);
     const uint64_t chunks = (P.n_slots + chunk - 1) / chunk;
     if (P.n_slots < 0xFFFFFFFFull && q < kPersistentMaxItems && chunks <= 4096) {
       P.wavefront = true;
@@ -1324,11 +1337,14 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
     WfArgs W{};
     if (P.wavefront) {
       const uint64_t levels = (uint64_t)P.F.max_depth + 1u, pairs = wf_pairs(c, P.F.light_spp);
-      const uint64_t q = levels * pairs * (P.wf_chunk + 8u);  // (+ the last band's padding, wf_q)
+      const uint64_t q = levels * pairs * (P.wf_chunk + kWfPad);  // (+ the bands' padding, wf_q)
+      const bool compact = wf_compact(c);
+      const uint64_t cnt_bytes = levels * ((P.wf_chunk + kWfPad) / 64u + 8u) + 4u;
       if (c->d_wf_rays_s[slot].fit(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_nl_s[slot].fit(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_occ_s[slot].fit(std::max<uint64_t>(q, 1)) == hipSuccess &&
-          c->d_wf_lvl_s[slot].fit(sizeof(float4) * levels * P.wf_chunk) == hipSuccess) {
+          c->d_wf_lvl_s[slot].fit(sizeof(float4) * levels * P.wf_chunk) == hipSuccess &&
+          (!compact || c->d_wf_cnt_s[slot].fit(cnt_bytes) == hipSuccess)) {
         wavefront = true;
         W.rays = c->d_wf_rays_s[slot].as<float4>();
         W.rays_b = W.rays + std::max<uint64_t>(q, 1);
@@ -1339,9 +1355,13 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         W.levels = (int)levels;
         W.grid = c->accel == DRT_ACCEL_GRID ? 1 : 0;
         W.inorder = P.aa_chain ? 0 : 1;
+        W.compact = compact ? 1 : 0;
+        W.cnt = compact ? c->d_wf_cnt_s[slot].as<uint8_t>() : nullptr;
       } else {
         (void)hipGetLastError();
-        for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot]}) b->release();
+        for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot],
+                          &c->d_wf_cnt_s[slot]})
+          b->release();
       }
     }
     FrameArgs F1 = P.F;  // pass 1: the pixels' closest-hit chains, samples in order (AA: any order)
@@ -1412,6 +1432,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       // 6 % slower with them and keeps 1 (profiles/r05_ab_wavefront_bands.jsonl)
       W.bands = env_int("DRT_WAVEFRONT_BANDS", W.grid ? 1 : 8) >= 8 ? 8 : 1;
       W.band = (W.n_slots + (uint32_t)W.bands - 1u) / (uint32_t)W.bands;
+      if (W.compact) W.band = (W.band + 255u) & ~255u;  // 64-slot groups, 256-query chunks, one (level, pair) row each
       launch_wf_gen(S, F2, W, st);
       DRT_HIP(c, hipGetLastError());
       const bool stage = k < (uint32_t)drt_ctx::kStageChunks && !c->stage_ev.empty();
@@ -1450,7 +1471,11 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         // the batched queries' 6 / 24 (7 / 16: 2 475-2 480, 7 / 10: 2 479-2 489, 8 / 16: 2 393-2 400,
         // 6 / 16: 2 431; C3 at 12 / 16: 3 430 / 3 425-3 427; r05_wavefront_knobs_*.jsonl)
         A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 12);
-        A.sparse = 1;
+        A.sparse = W.compact ? 2 : 1;
+        A.cnt = W.cnt;
+        A.levels = W.levels;
+        A.pairs = W.pairs;
+        A.band = W.band;
         A.parts = W.bands;
         A.part_len = W.bands == 8 ? part_len : (uint32_t)q;
         launch_trace_stream(S, A, true, c->tri_only, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);

@@ -2071,9 +2071,23 @@ __device__ bool wf_level_fw(const SceneArgs& S, const FrameArgs& F, const WfArgs
     V = neg(normalize(q.d));
   }
   V3 lightPos = mk(0, 0, 0);
+  // compact queries (WfArgs::compact): this wave's 64 slots are one group; its lanes with a query at this
+  // level take its first slots in lane order, and the group's count goes to W.cnt (by its lowest lane)
+  uint32_t crank = 0;
+  if (W.compact) {
+    const uint64_t act = __ballot(true), hb = __ballot(hit);
+    crank = __builtin_amdgcn_mbcnt_hi((uint32_t)(hb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hb, 0u));
+    const uint32_t lo = (uint32_t)__builtin_ctzll(act), lane = threadIdx.x & 63u;
+    if (lane == lo) {
+      const uint32_t b = slot / W.band, g = (slot - b * W.band) >> 6;
+      W.cnt[((size_t)b * (uint32_t)W.levels + (uint32_t)l) * (W.band >> 6) + g] = (uint8_t)__popcll(hb);
+    }
+  }
   for (int j = 0, u = 0; j < F.light_spp * S.n_lights; j++) {  // setup_shadow for every pair the light loop visits
     if (!wf_pair_used(S, F, j)) continue;
-    const size_t qi = wf_q(W, l, u++, slot);
+    const size_t qi = wf_q(W, l, u, slot);
+    const size_t qc = wf_q(W, l, u, slot & ~63u) + crank;  // (compact) the query's packed slot
+    u++;
     float4 ra = make_float4(0.f, 0.f, 0.f, -1.0f), rb = make_float4(0.f, 0.f, 0.f, 0.f);
     float2 nlv = make_float2(0.f, 0.f);
     if (hit) {
@@ -2087,11 +2101,16 @@ __device__ bool wf_level_fw(const SceneArgs& S, const FrameArgs& F, const WfArgs
       const V3 so = add(hitP, mul(N, 1e-4f));
       const V3 sd = W.grid ? normalize(Lv) : normalize(Ls);
       ra = make_float4(so.x, so.y, so.z, W.grid ? length(Lv) : shadow_threshold(length(Ls)));
-      rb = make_float4(sd.x, sd.y, sd.z, 0.0f);
+      rb = make_float4(sd.x, sd.y, sd.z, W.compact ? __uint_as_float((uint32_t)qi) : 0.0f);
       nlv = make_float2(NdotL, NdotH);
     }
-    wf_st(&W.rays[qi], ra);
-    wf_st(&W.rays_b[qi], rb);
+    if (!W.compact) {
+      wf_st(&W.rays[qi], ra);
+      wf_st(&W.rays_b[qi], rb);
+    } else if (hit) {
+      wf_st(&W.rays[qc], ra);
+      wf_st(&W.rays_b[qc], rb);
+    }
     wf_st(&W.nl[qi], nlv);
   }
   if (!hit) return false;
@@ -2617,6 +2636,9 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
   // from that wave-private range: one counter word serves only ~90 dequeues/us
   // (MI355X_MICROARCH.md, dequeue), so a claim per refill would cap the kernel near 1 Gquery/s.
   uint32_t chunk_next = 0, chunk_end = 0;  // wave-uniform
+  // sparse 2 (compact queries): chunk_next / chunk_end count the chunk's queries, chunk_base is its first
+  // slot and chunk_cnt its four 64-slot groups' counts (one byte each)
+  uint32_t chunk_base = 0, chunk_cnt = 0;  // wave-uniform
   bool exhausted = false;                  // wave-uniform: every partition's counter is past its end
   // partitions (TraceArgs::parts): a wave starts on its XCD's (HW_REG_XCC_ID), as path_persistent does
   uint32_t part = A.parts > 1 ? (__builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u) % (uint32_t)A.parts : 0u;
@@ -2637,6 +2659,15 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
         base = __shfl(base, 0, 64) + pbeg;
         chunk_next = base;
         chunk_end = base < pend ? min(base + kTraceChunk, pend) : base;
+        if (A.sparse == 2) {  // the chunk's four group counts (band slots are a multiple of 256: one row)
+          chunk_base = base;
+          chunk_next = chunk_end = 0;
+          if (base < pend) {
+            const uint32_t row = base / A.band, o0 = base - row * A.band, bl = row / (uint32_t)A.pairs;
+            chunk_cnt = *(const uint32_t*)(A.cnt + (size_t)bl * (A.band >> 6) + (o0 >> 6));
+            chunk_end = (chunk_cnt & 0xffu) + ((chunk_cnt >> 8) & 0xffu) + ((chunk_cnt >> 16) & 0xffu) + (chunk_cnt >> 24);
+          }
+        }
         if (base + kTraceChunk >= pend) {  // this partition is claimed: the next one
           part = part + 1u == (uint32_t)A.parts ? 0u : part + 1u;
           if (++parts_done == (uint32_t)A.parts) exhausted = true;
@@ -2646,14 +2677,21 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
         const uint32_t it = chunk_next + rank;
         if (it < chunk_end) {
+          uint32_t qs = it;  // the query's slot
+          if (A.sparse == 2) {  // the it-th query of the chunk: group j's (it - its first query)-th slot
+            const uint32_t p1 = chunk_cnt & 0xffu, p2 = p1 + ((chunk_cnt >> 8) & 0xffu), p3 = p2 + ((chunk_cnt >> 16) & 0xffu);
+            const uint32_t j = (it >= p1 ? 1u : 0u) + (it >= p2 ? 1u : 0u) + (it >= p3 ? 1u : 0u);
+            const uint32_t pre = j == 0u ? 0u : (j == 1u ? p1 : (j == 2u ? p2 : p3));
+            qs = chunk_base + 64u * j + (it - pre);
+          }
           // (interleaved records: rays_b = rays + 1, stride 2; or two arrays, stride 1)
-          const size_t at = (size_t)it * (uint32_t)A.stride;
+          const size_t at = (size_t)qs * (uint32_t)A.stride;
           const float4 a = wf_ld(&A.rays[at]);
           // (an empty slot is thr < 0, wf_mark_empty; a NaN range is a query, answered 0, as MODE_QSTREAM
           // answers it — ADVICE r5: skipping it left a stale answer in occ_out)
-          if (!A.sparse || !(a.w < 0.0f)) {
+          if (A.sparse != 1 || !(a.w < 0.0f)) {
           const float4 b = wf_ld(&A.rays_b[at]);
-          L.item = it;
+          L.item = A.sparse == 2 ? __float_as_uint(b.w) : it;  // (compact: the answer goes to the query's own slot)
           L.q = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
           L.thr = a.w;
           L.best_t = 3.402823466e+38f;
@@ -2675,7 +2713,7 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
         }
       }
       chunk_next = min(chunk_next + (uint32_t)n_want, chunk_end);
-      if (!A.sparse) break;
+      if (A.sparse != 1) break;
       want = __ballot(L.item == kNoItem);
       n_want = __popcll(want);
       if (n_want < A.refill_min || (exhausted && chunk_next >= chunk_end)) break;
@@ -2723,6 +2761,33 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
 // setup_shadow's light point, ray and Phong factors per (level, light pair), the unshadowed terms added
 // in pair order, the depth cut, and the mirror unwind.
 // ------------------------------------------------------------------------------------------
+// The sample's primary ray and light sample (seq_start_sample, MODE_AREPLAY / MODE_REPLAY); an in-order
+// frame's lens draw from its recorded stream position `rk`.
+__device__ __forceinline__ void wf_primary(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, const Item& it,
+                                           uint32_t g, uint32_t pmix, uint32_t& rk, RayP& q, V3& ls) {
+  if (F.spp > 0) {
+    const uint32_t pixel = g / (uint32_t)F.nsub;
+    float rx, ry, sx, sy;
+    const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + it.sub] : shuffle_source(F, pmix, it.sub);
+    sample_prologue_at(F, pmix, it.sub, pos, rx, ry, sx, sy);
+    const float px = (float)it.x + rx, py = (float)it.y + ry;
+    if (W.inorder && F.dof) {
+      KRng rng{F.seed, pmix, rk};
+      q = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
+      rk = rng.k;
+    } else {
+      q = primary_ray(S, px, py);
+    }
+    ls = mk(sx, sy, 0.0f);
+  } else {
+    const int sb = it.sub;
+    q = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
+    ls = F.grid_res ? mk(((float)(sb % F.grid_size) + 0.5f) / (float)F.grid_size,
+                         ((float)(sb / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
+                    : mk(0.5f, 0.5f, 0.0f);
+  }
+}
+
 __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, WfArgs W) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // the slot's place in this chunk's buffers
   if (slot >= W.band * (uint32_t)W.bands) return;
@@ -2732,58 +2797,39 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
   Item it{0, 0, 0, false};
   if (in) it = decode_item(F, S.res_x, S.res_y, g, F.nsub);
   int l = 0;  // the first level without shadow queries
+#ifndef DRT_WF_PIECEWISE
+  // every lane runs every level (padding lanes too): the query stores are whole-wave, and a compact
+  // group's ballots see all 64 lanes
+  RayP q{};
+  V3 ls = mk(0, 0, 0);
+  uint32_t rk = 0, rec = 0, pmix = 0;
+  if (it.valid) {
+    rec = F.chain_div > 1 ? (g - (uint32_t)it.sub) / (uint32_t)F.chain_div : g;
+    pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
+    rk = W.inorder ? F.skel_rk[g] : 0u;
+    wf_primary(S, F, W, it, g, pmix, rk, q, ls);
+  }
+  bool live = it.valid;
+  for (int lv = 0; lv <= md; lv++) {
+    uint2 h = make_uint2(0u, 0xFFFFFFFFu);
+    if (live) h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)lv];
+    const bool hit = live && h.y != 0xFFFFFFFFu;
+    RayP next;
+    const bool more = wf_level_fw(S, F, W, slot, lv, q, live, hit, __uint_as_float(h.x), h.y, ls, pmix, rk, next);
+    live = more;
+    if (more) q = next;
+  }
+  l = W.levels;
+#else
   if (it.valid) {
     const uint32_t rec = F.chain_div > 1 ? (g - (uint32_t)it.sub) / (uint32_t)F.chain_div : g;
     const uint32_t pmix = (uint32_t)(it.y * S.res_x + it.x) * 0x9E3779B9u;
     // an in-order frame's keyed stream from the sample's recorded position (MODE_REPLAY); an AA / Whitted
     // frame draws nothing after the prologue (Q16)
     uint32_t rk = W.inorder ? F.skel_rk[g] : 0u;
-    // the sample's primary ray and light sample (seq_start_sample, MODE_AREPLAY / MODE_REPLAY)
     RayP q;
     V3 ls;
-    if (F.spp > 0) {
-      const uint32_t pixel = g / (uint32_t)F.nsub;
-      float rx, ry, sx, sy;
-      const int pos = F.perm ? (int)F.perm[(size_t)pixel * F.spp + it.sub] : shuffle_source(F, pmix, it.sub);
-      sample_prologue_at(F, pmix, it.sub, pos, rx, ry, sx, sy);
-      const float px = (float)it.x + rx, py = (float)it.y + ry;
-      if (W.inorder && F.dof) {
-        KRng rng{F.seed, pmix, rk};
-        q = primary_ray_lens(S, dvf(mul(rnd_unit_disk(rng), S.aperture), 2.0f), px, py);
-        rk = rng.k;
-      } else {
-        q = primary_ray(S, px, py);
-      }
-      ls = mk(sx, sy, 0.0f);
-    } else {
-      const int sb = it.sub;
-      q = primary_ray(S, (float)it.x + 0.5f, (float)it.y + 0.5f);
-      ls = F.grid_res ? mk(((float)(sb % F.grid_size) + 0.5f) / (float)F.grid_size,
-                           ((float)(sb / F.grid_size) + 0.5f) / (float)F.grid_size, 0.0f)
-                      : mk(0.5f, 0.5f, 0.0f);
-    }
-#ifndef DRT_WF_PIECEWISE
-    bool live = true;
-    for (int lv = 0; lv <= md; lv++) {  // every level, every lane: the query stores are whole-wave
-      uint2 h = make_uint2(0u, 0xFFFFFFFFu);
-      if (live) h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)lv];
-      const bool hit = live && h.y != 0xFFFFFFFFu;
-      RayP next;
-      const bool more = wf_level_fw(S, F, W, slot, lv, q, live, hit, __uint_as_float(h.x), h.y, ls, pmix, rk, next);
-      live = more;
-      if (more) q = next;
-    }
-    l = W.levels;
-  } else {
-    RayP q0{};
-    V3 ls0 = mk(0, 0, 0);
-    uint32_t rk0 = 0;
-    for (int lv = 0; lv <= md; lv++) {
-      RayP next;
-      (void)wf_level_fw(S, F, W, slot, lv, q0, false, false, 0.0f, 0u, ls0, 0u, rk0, next);
-    }
-    l = W.levels;
-#else
+    wf_primary(S, F, W, it, g, pmix, rk, q, ls);
     while (l <= md) {
       const uint2 h = F.skel_hits[(size_t)rec * (uint32_t)(md + 1) + (uint32_t)l];
       const bool hit = h.y != 0xFFFFFFFFu;
@@ -2793,8 +2839,8 @@ __global__ void __launch_bounds__(256) wf_gen_kernel(SceneArgs S, FrameArgs F, W
       if (!more) break;
       q = next;
     }
-#endif
   }
+#endif
   wf_mark_empty(W, l, slot);
 }
 

@@ -149,6 +149,12 @@ struct WfArgs {
   int inorder;       // an in-order (DoF / glossy) frame: keyed-stream draws from FrameArgs::skel_rk (MODE_REPLAY)
   int grid;       // Grid scene: queries as Grid::Traverse(Ray&) takes them (unit L, range |L|)
   int pairs;      // query slots per level: the (light, k) pairs the light loop visits (a point light: k = 0 only)
+  // compact (round 6, BVH): each 64-slot group's queries of a (level, pair) packed to the group's first
+  // slots, in lane order, with the query's own slot index in rays_b.w, and per (band, level, group) their
+  // count in cnt[(band * levels + level) * (band_slots / 64) + group] (band a multiple of 256), so that
+  // trace_stream hands out queries without reading empty slots (TraceArgs::sparse 2).  0: thr = -1 markers.
+  int compact;
+  uint8_t* cnt;
 };
 
 struct FrameArgs {
@@ -233,7 +239,12 @@ struct TraceArgs {
   uint8_t* occ_out;            // shadow: 1 if occluded
   unsigned long long* stats;   // ST_* counters (stats launches only)
   int refill_min;
-  int sparse;                  // shadow queries with thr < 0 are empty slots: skipped, occ_out not written
+  int sparse;                  // 1: shadow queries with thr < 0 are empty slots: skipped, occ_out not written;
+                               // 2: WfArgs::compact queries — per 256-query chunk four 64-slot group counts
+                               // (cnt), the answer written to the query's own slot (rays_b.w)
+  const uint8_t* cnt;          // sparse 2: WfArgs::cnt
+  int levels, pairs;           // sparse 2: the query array's shape [band][level][pair][band_slots]
+  uint32_t band;
   // work partitions: `parts` ranges of part_len queries, one claim counter each (64 B apart); a wave
   // starts on the range of its XCD and moves on when that one is claimed (parts 1: one counter)
   int parts;

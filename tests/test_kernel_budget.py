@@ -42,9 +42,10 @@ BUDGET = {
     # batched shadow queries (drt_trace_shadow) on the 4-ary shadow tree: 8 waves/SIMD, no spills
     # (round 5: 64 VGPRs with the two-array query records (TraceArgs::stride): 7 waves by the compiler's
     # count, down from 8)
-    "drt::trace_stream<true, 2, 6, false>": (64, 352, 7, 0),
+    # (round 6: the compact-query refill, TraceArgs::sparse 2: 67-69 VGPRs, still 7 waves)
+    "drt::trace_stream<true, 2, 6, false>": (72, 352, 7, 0),
     # the wavefront replay's shadow queries (round 5): 7 waves/SIMD of LDS stack, no spills
-    "drt::trace_stream<true, 2, 7, false>": (64, 352, 7, 0),
+    "drt::trace_stream<true, 2, 7, false>": (72, 352, 7, 0),
     # Grid stepper, AA frames (5 waves/SIMD: 96 VGPRs), and the two passes of the Grid headline's frame
     "drt::path_persistent<true, false, 0, 5, 1>": (96, 1844, 5, 79),
     "drt::path_persistent<true, false, 7, 5, 1>": (96, 8, 5, 1),
