@@ -4,7 +4,8 @@
 #      Grid configs (tools/pmc_configs.sh)
 #   Y: the PMC records of C4 and C2, every BASELINE config (tools/configs.sh, 10 steps, CPU baselines), the
 #      bench line and a rocprofv3 --kernel-trace --stats run of the same command (tools/gpu_check.sh, no tests)
-#   usage: bash tools/final_session.sh X|Y
+#   Z: Y without the PMC passes, plus the 2-rank multi-rank rehearsal (tools/multirank_check.sh)
+#   usage: bash tools/final_session.sh X|Y|Z
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
@@ -24,4 +25,17 @@ case "${1:-X}" in
     python tools/rocprof_union.py $OUT/prof --steps 20 --warmup 2 --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
     cat $OUT/rocprof_union.json
     ;;
+  Z)  # the head's bench evidence after a change that needs no new PMC records: Y without its PMC passes, plus
+      # the multi-rank rehearsal
+    CFG_STEPS=10 bash tools/configs.sh || exit $?
+    timeout -k 10 600 python bench.py --steps 20 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+    cut -c1-300 $OUT/bench.json
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
+        python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || exit $?
+    python tools/rocprof_union.py $OUT/prof --steps 20 --warmup 2 --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
+    cat $OUT/rocprof_union.json
+    NPROC=2 bash tools/multirank_check.sh || exit $?
+    ;;
+  *)
+    echo "unknown part $1"; exit 2 ;;
 esac
