@@ -25,6 +25,8 @@ void launch_trace_stream(const SceneArgs& S, const TraceArgs& A, bool shadow, bo
                          hipStream_t st);
 void launch_trace_prep(const float* rays, int n, int shadow, float4* out, hipStream_t st);
 void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
+void launch_grid_stream(const SceneArgs& S, const TraceArgs& A, bool tri_only, bool stats, int waves, int walk, int pairs,
+                        hipStream_t st);
 void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
 void launch_wf_combine_reduce(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, const ReduceArgs& R,
                               hipStream_t st);
@@ -950,14 +952,16 @@ struct Plan {
 static void note_last_path_ms(drt_ctx* c);
 // Query slots a chunk's buffers hold beyond its sample slots: each of <= 8 bands rounded up to 256 slots.
 constexpr uint64_t kWfPad = 8u * 256u;
-// BVH wavefront frames pack each 64-slot group's queries (WfArgs::compact, round 6); DRT_WAVEFRONT_COMPACT=0
-// keeps the thr = -1 markers.  The Grid's query stream (MODE_QSTREAM) reads the marker layout.
+// Wavefront frames pack each 64-slot group's queries (WfArgs::compact, round 6): the BVH's trace_stream and
+// the Grid's grid_stream refill from the group counts.  DRT_WAVEFRONT_COMPACT=0 keeps the thr = -1 markers
+// (and on the Grid the path kernel's MODE_QSTREAM, as DRT_GRID_STREAM=0 does).
 static bool wf_compact(const drt_ctx* c) {
 #ifdef DRT_WF_PIECEWISE
   (void)c;
   return false;
 #else
-  return c->accel == DRT_ACCEL_BVH && env_int("DRT_WAVEFRONT_COMPACT", 1) != 0;
+  if (env_int("DRT_WAVEFRONT_COMPACT", 1) == 0) return false;
+  return c->accel == DRT_ACCEL_BVH || (c->accel == DRT_ACCEL_GRID && env_int("DRT_GRID_STREAM", 1) != 0);
 #endif
 }
 // Shadow-query slots per level of a wavefront replay: the (light, k) pairs the light loop visits — every
@@ -1429,8 +1433,10 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       W.n_slots = (uint32_t)std::min<uint64_t>(P.wf_chunk, P.n_slots - W.slot0);
       // XCD bands (wf_q): DRT_WAVEFRONT_BANDS (1 or 8) consecutive ranges of the chunk's sample slots, each
       // streamed first by one XCD.  BVH 8: headline +0.2 %, C3 +0.8 %; the Grid's MODE_QSTREAM measured
-      // 6 % slower with them and keeps 1 (profiles/r05_ab_wavefront_bands.jsonl)
-      W.bands = env_int("DRT_WAVEFRONT_BANDS", W.grid ? 1 : 8) >= 8 ? 8 : 1;
+      // 6 % slower with them and keeps 1 (profiles/r05_ab_wavefront_bands.jsonl); the Grid's grid_stream
+      // (round 6, compact queries) gains 2.7 % with them: 2 079 / 2 066 against 2 023 / 2 020 Mrays/s
+      // (profiles/r06_ab_grid_stream.jsonl)
+      W.bands = env_int("DRT_WAVEFRONT_BANDS", (W.grid && !W.compact) ? 1 : 8) >= 8 ? 8 : 1;
       W.band = (W.n_slots + (uint32_t)W.bands - 1u) / (uint32_t)W.bands;
       if (W.compact) W.band = (W.band + 255u) & ~255u;  // 64-slot groups, 256-query chunks, one (level, pair) row each
       launch_wf_gen(S, F2, W, st);
@@ -1440,7 +1446,28 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       const uint64_t q = (uint64_t)W.levels * (uint64_t)W.pairs * W.band * (uint64_t)W.bands;
       const uint32_t part_len = (uint32_t)((uint64_t)W.levels * W.pairs * W.band);
       unsigned int* counter = d_counter.as<unsigned int>() + 256u * (1u + k);
-      if (q && W.grid) {
+      if (q && W.grid && W.compact) {
+        // the Grid's shadow queries on its own streaming kernel (grid_stream, round 6): the Grid stepper,
+        // refilled from the compact query array like trace_stream
+        TraceArgs A{};
+        A.rays = W.rays;
+        A.rays_b = W.rays_b;
+        A.stride = 1;
+        A.n = (uint32_t)q;
+        A.counter = counter;
+        A.occ_out = W.occ;
+        A.stats = F2.stats;
+        A.refill_min = env_int("DRT_WAVEFRONT_GRID_REFILL_MIN", 16);
+        A.sparse = 2;
+        A.cnt = W.cnt;
+        A.levels = W.levels;
+        A.pairs = W.pairs;
+        A.band = W.band;
+        A.parts = W.bands;
+        A.part_len = W.bands == 8 ? part_len : (uint32_t)q;
+        launch_grid_stream(S, A, c->tri_only, stats, env_int("DRT_WAVEFRONT_GRID_WAVES", 7), F2.grid_walk, F2.grid_pairs, st);
+        DRT_HIP(c, hipGetLastError());
+      } else if (q && W.grid) {
         // the Grid's shadow queries on its persistent stepper (MODE_QSTREAM): Grid::Traverse(Ray&)'s answer
         // is tied to the cells its walk visits, so they stay on the Grid
         FrameArgs FQ = F2;

@@ -2754,6 +2754,89 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
 }
 
 // ------------------------------------------------------------------------------------------
+// The Grid's wavefront shadow queries as their own streaming kernel (round 6): `Grid::Traverse(Ray&)`
+// (grid.cpp:309-358) on the persistent stepper's grid_step, one query per lane, refilled from the compact
+// query array as trace_stream refills (TraceArgs::sparse 2: a 256-query claim's four 64-slot group counts,
+// the query's own slot in rays_b.w, the answer written there).  It replaces MODE_QSTREAM of the path
+// kernel, whose lanes loaded every empty (thr < 0) slot of the marker layout to find the queries.
+// ------------------------------------------------------------------------------------------
+template <bool TRI_ONLY, int WAVES, bool STATS>
+__global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs A, int walk, int pairs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_bytes[];
+  for (int w = threadIdx.x; w < S.gmacro_words; w += 256) ((LdsU32*)lds_bytes)[w] = S.gmacro[w];
+  __syncthreads();
+  Counters C;
+  for (int s = 0; s < ST_COUNT; s++) C.v[s] = 0;
+  Lane L;
+  L.item = kNoItem;
+  L.fl = 0u;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t chunk_next = 0, chunk_end = 0, chunk_base = 0, chunk_cnt = 0;  // wave-uniform (as trace_stream)
+  bool exhausted = false;
+  uint32_t part = A.parts > 1 ? (__builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u) % (uint32_t)A.parts : 0u;
+  uint32_t parts_done = 0;
+  while (true) {
+    const uint64_t idle = __ballot(L.item == kNoItem);
+    const int n_idle = __popcll(idle);
+    if (n_idle >= A.refill_min || n_idle == 64) {
+      while (chunk_next >= chunk_end && !exhausted) {  // claim 256 query slots of the wave's partition
+        const uint32_t pbeg = part * A.part_len, pend = min(pbeg + A.part_len, A.n);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(A.counter + 16u * part, kTraceChunk);
+        base = __shfl(base, 0, 64) + pbeg;
+        chunk_base = base;
+        chunk_next = chunk_end = 0;
+        if (base < pend) {  // the chunk's four group counts (one row of the query array)
+          const uint32_t row = base / A.band, o0 = base - row * A.band, bl = row / (uint32_t)A.pairs;
+          chunk_cnt = *(const uint32_t*)(A.cnt + (size_t)bl * (A.band >> 6) + (o0 >> 6));
+          chunk_end = (chunk_cnt & 0xffu) + ((chunk_cnt >> 8) & 0xffu) + ((chunk_cnt >> 16) & 0xffu) + (chunk_cnt >> 24);
+        }
+        if (base + kTraceChunk >= pend) {
+          part = part + 1u == (uint32_t)A.parts ? 0u : part + 1u;
+          if (++parts_done == (uint32_t)A.parts) exhausted = true;
+        }
+      }
+      if (L.item == kNoItem) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        const uint32_t it = chunk_next + rank;
+        if (it < chunk_end) {
+          const uint32_t p1 = chunk_cnt & 0xffu, p2 = p1 + ((chunk_cnt >> 8) & 0xffu), p3 = p2 + ((chunk_cnt >> 16) & 0xffu);
+          const uint32_t j = (it >= p1 ? 1u : 0u) + (it >= p2 ? 1u : 0u) + (it >= p3 ? 1u : 0u);
+          const uint32_t pre = j == 0u ? 0u : (j == 1u ? p1 : (j == 2u ? p2 : p3));
+          const size_t at = (size_t)(chunk_base + 64u * j + (it - pre));
+          const float4 a = wf_ld(&A.rays[at]);
+          const float4 b = wf_ld(&A.rays_b[at]);
+          L.item = __float_as_uint(b.w);
+          L.fl = 0u;
+          // a shadow ray that misses the grid box counts as shadowed (grid.cpp:323-324, Q8): start_query
+          start_query<STATS, ACC_GRID>(S, L, make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z)), true, a.w, C);
+        }
+      }
+      chunk_next = min(chunk_next + (uint32_t)n_idle, chunk_end);
+    }
+    const bool in_trav = L.item != kNoItem && (L.fl & LF_TRAV);
+    const uint64_t trav = __ballot(in_trav);
+    if (trav) {
+      if (STATS && lane == 0) C.v[ST_WAVE_NODE_ITERS]++;
+      if (in_trav) grid_step<TRI_ONLY, STATS>(S, L, C, (const LdsU32*)lds_bytes, walk, pairs);
+    }
+    if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: its answer to the query's own slot
+      wf_st(&A.occ_out[L.item], (uint8_t)((L.fl & LF_HIT) ? 1 : 0));
+      L.item = kNoItem;
+    } else if (!trav && exhausted && chunk_next >= chunk_end) {
+      break;
+    }
+  }
+  if (STATS) {
+    for (int s = 0; s < ST_COUNT; s++) {
+      unsigned long long v = C.v[s];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if (lane == 0 && v) atomicAdd(&A.stats[s], v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Wavefront replay (round 5; drt_kernels.hpp WfArgs): an AA / Whitted two-pass BVH frame without
 // refraction, pass 2 as three launches — wf_gen, trace_stream over every shadow query of the frame,
 // wf_combine — instead of the persistent MODE_AREPLAY kernel, whose waves interleave shading (a third
@@ -3219,6 +3302,35 @@ static void launch_stream_k(const SceneArgs& S, const TraceArgs& A, int waves, h
   else if (waves == 7) launch_stream_w<T, K, 7, ST>(S, A, st);
   else launch_stream_w<T, K, 6, ST>(S, A, st);
 }
+template <bool T, int W, bool ST>
+static void launch_grid_stream_w(const SceneArgs& S, const TraceArgs& A, int walk, int pairs, hipStream_t st) {
+  const size_t lds = kMacroBits / 8;
+  static int grid = 0;  // resident blocks across the device (per instantiation)
+  if (!grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)grid_stream<T, W, ST>, 256, lds);
+    grid = std::max(1, cus) * std::max(1, per_cu);
+  }
+  const uint64_t need = ((uint64_t)A.n + 255) / 256;
+  const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)grid));
+  hipLaunchKernelGGL((grid_stream<T, W, ST>), dim3(blocks), dim3(256), lds, st, S, A, walk, pairs);
+}
+// the Grid's compact wavefront shadow queries (grid_stream); waves per SIMD 5, 6 or 7
+void launch_grid_stream(const SceneArgs& S, const TraceArgs& A, bool tri_only, bool stats, int waves, int walk, int pairs,
+                        hipStream_t st) {
+  if (tri_only) {
+    if (stats) launch_grid_stream_w<true, 7, true>(S, A, walk, pairs, st);
+    else if (waves <= 5) launch_grid_stream_w<true, 5, false>(S, A, walk, pairs, st);
+    else if (waves == 6) launch_grid_stream_w<true, 6, false>(S, A, walk, pairs, st);
+    else launch_grid_stream_w<true, 7, false>(S, A, walk, pairs, st);
+  } else {
+    if (stats) launch_grid_stream_w<false, 7, true>(S, A, walk, pairs, st);
+    else launch_grid_stream_w<false, 7, false>(S, A, walk, pairs, st);
+  }
+}
+
 void launch_trace_stream(const SceneArgs& S, const TraceArgs& A, bool shadow, bool tri_only, bool stats, int waves,
                          hipStream_t st) {
   if (tri_only) {

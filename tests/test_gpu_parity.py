@@ -947,7 +947,10 @@ def test_whitted_two_pass_frame_equals_one_pass(drt, renderer, monkeypatch, acce
     # XCD bands of the query array (DRT_WAVEFRONT_BANDS=8; chunk -1: bands alone)
     ("bvh", 16, "point", 1, 4, 0, -1), ("grid", 9, "quad", 1, 3, 0.2, -1),
     # a scene without lights: no shadow query at all, the frame is the mirrored background
-    ("bvh", 16, "none", 1, 4, 0, 0), ("grid", 4, "none", 1, 2, 0, 0)])
+    ("bvh", 16, "none", 1, 4, 0, 0), ("grid", 4, "none", 1, 2, 0, 0),
+    # round 6: the marker layout instead of the compact queries (chunk -2: DRT_WAVEFRONT_COMPACT=0; the Grid
+    # then runs MODE_QSTREAM instead of grid_stream)
+    ("bvh", 16, "quad", 1, 4, 0, -2), ("grid", 16, "quad", 1, 4, 0, -2), ("grid", 0, "point", 1, 3, 0.2, -2)])
 def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, accel, spp, first, light_spp, md, rough,
                                                    chunk):
     """Pass 2 of an AA / Whitted two-pass BVH frame as a wavefront (round 5; drt_kernels.hpp WfArgs):
@@ -959,7 +962,11 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, a
     in-order (glossy) frames whose lens and reflectDir draws wf_gen takes from the recorded stream
     positions, pass 2 in chunks of sample slots (DRT_WAVEFRONT_CHUNK_SLOTS, a partial last chunk), and the
     query array in 8 XCD bands (DRT_WAVEFRONT_BANDS, a padded last band).
-    On the Grid the queries run on its persistent stepper (MODE_QSTREAM), with the same cell work."""
+    On the Grid the queries run on its stepper (round 6: grid_stream over the compact queries; MODE_QSTREAM
+    over the marker layout with DRT_WAVEFRONT_COMPACT=0), with the same cell work."""
+    if chunk == -2:
+        monkeypatch.setenv("DRT_WAVEFRONT_COMPACT", "0")
+        chunk = 0
     if chunk > 0:
         monkeypatch.setenv("DRT_WAVEFRONT_CHUNK_SLOTS", str(chunk))
     # (BVH frames default to 8 XCD bands, Grid frames to 1): chunked frames run with 8, so the last band
