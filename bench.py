@@ -477,7 +477,13 @@ def main():
                                 ("replay", float(np.mean(pass2_ms)), b2, pmc_passes[1])):
             row = {"pass": name, "ms": round(ms, 3), "bytes": int(b), "achieved": round(b / (ms * 1e-3) / 1e9, 1)}
             if name == "replay":
-                row["kernels"] = ("wf_gen + trace_stream<shadow> + wf_combine" if wavefront else
+                # the stream kernel: trace_stream (BVH), grid_stream over the compact queries (Grid, round 6) or
+                # the path kernel's MODE_QSTREAM over the marker layout (DRT_GRID_STREAM=0 / DRT_WAVEFRONT_COMPACT=0)
+                compact = os.environ.get("DRT_WAVEFRONT_COMPACT", "1") != "0" and (
+                    args.accel == "bvh" or os.environ.get("DRT_GRID_STREAM", "1") != "0")
+                stream_name = ("trace_stream<shadow>" if args.accel == "bvh" else
+                               "grid_stream" if compact else "path_persistent<GRID> query stream")
+                row["kernels"] = (f"wf_gen + {stream_name} + wf_combine" if wavefront else
                                   f"path_persistent<{args.accel.upper()}> replay")
                 if stage_ms:
                     # each launch of the wavefront pass 2 on its own: its device time in
@@ -490,14 +496,15 @@ def main():
                     n_quad = 1 if args.scene == "synthetic" else 2
                     pairs = n_quad * max(1, args.light_spp) + 1
                     slots = plan["sample_slots"]
-                    if args.accel == "bvh":  # compact queries: records of the real queries only (WfArgs::compact)
+                    if compact:  # compact queries: records of the real queries only (WfArgs::compact)
                         gen_b = mine["shadow_rays"] * 32 + slots * levels * (pairs * 8 + 16)
-                    else:  # the Grid's query stream reads the marker layout: every (level, pair) slot
+                    else:  # the marker layout: every (level, pair) slot
                         gen_b = slots * levels * (pairs * 40 + 16)
+                    if args.accel == "bvh" and os.environ.get("DRT_SHADOW_CLIMB", "1") != "0":
+                        gen_b += mine["shadow_rays"] * 4  # each query's start record (TraceArgs::start)
                     comb_b = slots * levels * (pairs * 9 + 16) + 12 * slots // max(1, args.spp)
                     la = {}
-                    for key, label, bb in (("wf_gen", "wf_gen", gen_b), ("stream", "trace_stream" if args.accel == "bvh"
-                                            else "path_persistent<GRID> query stream", b),
+                    for key, label, bb in (("wf_gen", "wf_gen", gen_b), ("stream", stream_name, b),
                                            ("wf_combine", "wf_combine (reduce folded in)", comb_b)):
                         lm = float(stage_ms[key])
                         e = {"kernel": label, "ms": round(lm, 3), "bytes": int(bb),
@@ -565,7 +572,8 @@ def main():
                      "pmc": pmc or None,
                      "two_level_model": model,
                      "kernel": f"path_persistent<{args.accel.upper()}>" + (
-                         " closest chain + wavefront replay (wf_gen, trace_stream, wf_combine)" if wavefront else
+                         (" closest chain + wavefront replay (wf_gen, trace_stream, wf_combine)" if args.accel == "bvh" else
+                          " closest chain + wavefront replay (wf_gen, grid_stream, wf_combine)") if wavefront else
                          " closest chain + replay" if passes == 2 else ""),
                      "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),

@@ -3,7 +3,7 @@
 tools/rocprof_union.py (roofline.kernel_ms against the trace) and tools/pmc_traffic.py (per-pass fabric
 bytes) must group a frame's dispatches the way run_frame issues them: the non-stats path_persistent
 dispatch of pass 1, then on the same stream / queue its second pass — the persistent replay
-(FrameMode 6 / 8 / 10) or the wavefront replay (wf_gen, the non-stats trace_stream or the Grid's
+(FrameMode 6 / 8 / 10) or the wavefront replay (wf_gen, the non-stats trace_stream, grid_stream or the Grid's
 MODE_QSTREAM dispatch, wf_combine; per chunk of sample slots).  Stats frames are skipped, and frames in
 flight interleave across streams.
 """
@@ -115,3 +115,36 @@ def test_rocprof_union_counts_the_folded_combine(tmp_path):
     r = json.loads(out)
     assert r["dispatches_per_frame"] == 4
     assert abs(r["kernel_ms_per_step_union"] - 20.0) < 0.01 and COMBR in r["kernels"]
+
+
+def test_profile_tools_count_grid_stream(tmp_path):
+    """Round 6: a Grid wavefront frame's shadow queries run on grid_stream (non-stats dispatch: last template
+    argument false); both tools count it as part of the frame, and skip the stats instantiation."""
+    import pmc_traffic
+
+    gs = "void drt::grid_stream<true, 7, false>(drt::SceneArgs, drt::TraceArgs, int, int)"
+    gs_st = "void drt::grid_stream<true, 7, true>(drt::SceneArgs, drt::TraceArgs, int, int)"
+    gchain_st = GCHAIN.replace("true, false", "true, true")
+    d = [x for x in frame(gchain_st, [GEN, gs_st, COMBR], 0, 0) if x[0] != REDUCE]
+    for k in range(2):  # 1 warmup + 1 timed
+        d += [x for x in frame(GCHAIN, [GEN, gs, COMBR], 0, 100_000_000 * (k + 1)) if x[0] != REDUCE]
+    write_trace(tmp_path / "t", d)
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "rocprof_union.py"), str(tmp_path / "t"), "--steps", "1",
+                          "--warmup", "1", "--settle", "0"], capture_output=True, text=True, check=True).stdout
+    r = json.loads(out)
+    assert r["frames"] == 2 and r["dispatches_per_frame"] == 4 and gs in r["kernels"] and gs_st not in r["kernels"]
+    assert abs(r["kernel_ms_per_step_union"] - 20.0) < 0.01
+
+    p = tmp_path / "p1"
+    p.mkdir()
+    rows = []
+    for did, (name, *_rest) in enumerate(d, 1):
+        rows.append({"Dispatch_Id": did, "Kernel_Name": name, "Queue_Id": 6, "Counter_Name": "WRITE_SIZE",
+                     "Counter_Value": 1.0 * did})
+    with open(p / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    c = pmc_traffic.dispatch_counters(p)
+    fr = pmc_traffic.last_frame(c)
+    assert [k[0] for k in fr] == [9, 10, 11, 12] and fr[2][1] == gs

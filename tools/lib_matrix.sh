@@ -17,7 +17,8 @@ d = json.load(open(sys.argv[3]))
 print(json.dumps({"label": sys.argv[1], "env": sys.argv[2], "value": d["value"], "ms_per_step": d["ms_per_step"],
                   "kernel_ms": d["roofline"]["kernel_ms"], "node_visits_per_ray": d["node_visits_per_ray"],
                   "bytes_per_ray": d["bytes_per_ray"], "shadow_tree": d.get("shadow_tree"), "simd_eff": d["simd_eff"],
-                  "cycle_share": d["cycle_share"], "cycles_per_iter": d.get("cycles_per_iter")}))
+                  "cycle_share": d["cycle_share"], "cycles_per_iter": d.get("cycles_per_iter"),
+                  "passes": d["roofline"].get("passes")}))
 PY
     tail -1 $OUT/lib_matrix.jsonl | cut -c1-150
     [ $rc -eq 0 ] || exit $rc

@@ -38,8 +38,8 @@ def dispatch_counters(pass_dir: Path):
 def last_frame(counters, sub=None):
     """Dispatch keys of the last timed frame: its non-stats path_persistent dispatch (pass 1, or the
     whole one-pass frame), then on the same queue its second pass — the persistent replay (FrameMode
-    6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the non-stats trace_stream or the Grid's
-    MODE_QSTREAM (11) dispatch, wf_combine_kernel or, reduce folded in, wf_combine_reduce_kernel; per chunk of sample slots).
+    6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the non-stats trace_stream, the Grid's
+    non-stats grid_stream or its MODE_QSTREAM (11) dispatch, wf_combine_kernel or, reduce folded in, wf_combine_reduce_kernel; per chunk of sample slots).
     With `sub`, the last dispatch whose name holds it."""
     if sub:
         keys = sorted(k for k in counters if sub in k[1])
@@ -56,7 +56,7 @@ def last_frame(counters, sub=None):
                 cur[q] = [k]
                 frames.append(cur[q])
         elif ("wf_gen_kernel" in name or "wf_combine" in name or
-              ("trace_stream<" in name and a and a[-1] == "false")) and cur.get(q) is not None:
+              (("trace_stream<" in name or "grid_stream<" in name) and a and a[-1] == "false")) and cur.get(q) is not None:
             cur[q].append(k)
     return frames[-1] if frames else []
 

@@ -34,7 +34,7 @@ def main():
     settle = settle or 0
     # A frame is its non-stats path_persistent dispatch plus, on the same stream, the dispatches of its
     # second pass: the persistent replay (FrameMode 6 / 8 / 10) or the wavefront replay (wf_gen_kernel, the
-    # non-stats trace_stream or the Grid's MODE_QSTREAM (11) dispatch, wf_combine_kernel or, reduce folded in, wf_combine_reduce_kernel; per chunk of
+    # non-stats trace_stream, the Grid's non-stats grid_stream or its MODE_QSTREAM (11) dispatch, wf_combine_kernel or, reduce folded in, wf_combine_reduce_kernel; per chunk of
     # sample slots).  Frames in flight interleave across streams.
     rows = []
     for f in Path(a.trace_dir).rglob("*kernel_trace.csv"):
@@ -56,7 +56,7 @@ def main():
                 cur[stream] = [(s0, e0, k)]
                 frames.append(cur[stream])
         elif ("wf_gen_kernel" in k or "wf_combine" in k or
-              ("trace_stream<" in k and targs[-1].strip() == "false")) and cur.get(stream) is not None:
+              (("trace_stream<" in k or "grid_stream<" in k) and targs[-1].strip() == "false")) and cur.get(stream) is not None:
             cur[stream].append((s0, e0, k))
     names = sorted({k for fr in frames for _, _, k in fr})
     P = max((len(fr) for fr in frames), default=1)
