@@ -500,8 +500,6 @@ def main():
                         gen_b = mine["shadow_rays"] * 32 + slots * levels * (pairs * 8 + 16)
                     else:  # the marker layout: every (level, pair) slot
                         gen_b = slots * levels * (pairs * 40 + 16)
-                    if args.accel == "bvh" and os.environ.get("DRT_SHADOW_CLIMB", "1") != "0":
-                        gen_b += mine["shadow_rays"] * 4  # each query's start record (TraceArgs::start)
                     comb_b = slots * levels * (pairs * 9 + 16) + 12 * slots // max(1, args.spp)
                     la = {}
                     for key, label, bb in (("wf_gen", "wf_gen", gen_b), ("stream", stream_name, b),

@@ -1013,35 +1013,6 @@ def test_wavefront_replay_equals_persistent_replay(drt, renderer, monkeypatch, a
         assert st[k] == st1[k], k
 
 
-@pytest.mark.parametrize("kw", [{}, {"light_spp": 4}, {"roughness": 0.1, "max_depth": 6}])
-def test_shadow_climb_does_not_change_the_frame(drt, renderer, monkeypatch, kw):
-    """Round 6: the wavefront's shadow queries start at the wide record above their hit's leaf and climb
-    (TraceArgs::start; DRT_SHADOW_CLIMB=0: every walk from the root).  Every leaf whose box the ray hits
-    is still reached and the leaf-box check decides as before, so on the 1M-triangle scene (AA, four
-    quad-light samples, glossy in-order) the frame is bit-identical to the root walk's, with the same
-    rays and shadow queries; only the shadow tree's visit counts move (printed)."""
-    import bench
-
-    s = drt.Scene()
-    bench.populate(s, bench.synthetic_triangles(1_000_000), 96, 4)
-    s.build()
-    renderer.upload(s)
-    assert renderer.plan(renderer.frame_params(seed=9, **kw))["wavefront"]
-    out = {}
-    for climb in ("0", "1"):
-        monkeypatch.setenv("DRT_SHADOW_CLIMB", climb)
-        out[climb] = (bits(renderer.render(seed=9, stats=True, **kw)), renderer.stats())
-    (ref, rst), (img, st) = out["0"], out["1"]
-    np.testing.assert_array_equal(img, ref)
-    for k in ("closest_rays", "shadow_rays", "closest_inner", "closest_leaf", "closest_prims", "samples",
-              "wide_shadow_rays"):
-        assert st[k] == rst[k], k
-    n = max(1, st["wide_shadow_rays"])
-    print(f"\nper wide query: inner {rst['wide_inner'] / n:.2f} -> {st['wide_inner'] / n:.2f}, leaf "
-          f"{rst['wide_leaf'] / n:.2f} -> {st['wide_leaf'] / n:.2f}, prims {rst['wide_prims'] / n:.2f} -> "
-          f"{st['wide_prims'] / n:.2f}")
-
-
 @pytest.mark.parametrize("accel,spp", [("bvh", 4), ("grid", 4), ("bvh", 0), ("grid", 0)])
 def test_refraction_two_pass_frame_equals_one_pass(drt, oracle_mod, renderer, tmp_path, monkeypatch, accel, spp):
     """AA and Whitted frames of scenes WITH a refracting material (glass spheres, trans 1) run in two
