@@ -5,7 +5,8 @@
 #   Y: the PMC records of C4 and C2, every BASELINE config (tools/configs.sh, 10 steps, CPU baselines), the
 #      bench line and a rocprofv3 --kernel-trace --stats run of the same command (tools/gpu_check.sh, no tests)
 #   Z: Y without the PMC passes, plus the 2-rank multi-rank rehearsal (tools/multirank_check.sh)
-#   usage: bash tools/final_session.sh X|Y|Z
+#   G: the Grid PMC record after grid_stream + Z's bench evidence; H: tests, smoke, multi-rank, shard scaling
+#   usage: bash tools/final_session.sh X|Y|Z|G|H
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
@@ -35,6 +36,22 @@ case "${1:-X}" in
     python tools/rocprof_union.py $OUT/prof --steps 20 --warmup 2 --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
     cat $OUT/rocprof_union.json
     NPROC=2 bash tools/multirank_check.sh || exit $?
+    ;;
+  G)  # after grid_stream: the Grid's PMC record (its pass-2 stream now counted), then Z's bench evidence with
+      # that record in the database the bench reads
+    cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
+    PMC_ONLY="grid" PMC_DB=$OUT/pmc_traffic.json bash tools/pmc_configs.sh || exit $?
+    cp $OUT/pmc_traffic.json profiles/pmc_traffic.json
+    CFG_STEPS=10 bash tools/configs.sh || exit $?
+    timeout -k 10 600 python bench.py --steps 20 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || exit $?
+    cut -c1-300 $OUT/bench.json
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
+        python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || exit $?
+    python tools/rocprof_union.py $OUT/prof --steps 20 --warmup 2 --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
+    cat $OUT/rocprof_union.json
+    ;;
+  H)  # the parity tests, smoke, the multi-rank rehearsal and the shard scaling at the head
+    bash tools/session.sh tests smoke mr:2 "shards:--steps 40 --pipe 2" || exit $?
     ;;
   *)
     echo "unknown part $1"; exit 2 ;;
