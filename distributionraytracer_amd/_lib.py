@@ -109,6 +109,7 @@ SIGNATURES = {
     "drt_set_camera": (C.c_int, [_vp, C.POINTER(DrtCamera)]),
     "drt_upload_bvh": (C.c_int, [_vp, _vp, C.c_uint32, _u32, C.c_uint32]),
     "drt_upload_grid": (C.c_int, [_vp, _i32, _f, _f, _i64, _i32, C.c_int64]),
+    "drt_upload_grid_shadow_bvh": (C.c_int, [_vp, _vp, C.c_uint32, _u32, C.c_uint32]),
     "drt_render": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _f]),
     "drt_shard_layout": (C.c_int, [_vp, C.POINTER(DrtFrameParams), _i64, _i64]),
     "drt_plan_frame": (C.c_int, [_vp, C.POINTER(DrtFrameParams), C.POINTER(DrtFramePlan)]),

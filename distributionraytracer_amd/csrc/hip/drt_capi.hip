@@ -27,6 +27,8 @@ void launch_trace_prep(const float* rays, int n, int shadow, float4* out, hipStr
 void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
 void launch_grid_stream(const SceneArgs& S, const TraceArgs& A, bool tri_only, bool stats, int waves, int walk, int pairs,
                         hipStream_t st);
+void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const TraceArgs& A, bool stats, int waves,
+                             hipStream_t st);
 void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
 void launch_wf_combine_reduce(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, const ReduceArgs& R,
                               hipStream_t st);
@@ -122,6 +124,14 @@ struct drt_ctx {
   DevBuf d_gprims, d_cell_pos;  // indexed Grid layout (experiment): Morton-ordered records, per-reference positions
   DevBuf d_cell_tris, d_cell_tpos;  // triangle scenes: 40-B triangles in pairs per cell, pair-aligned cell starts
   int gmacro_shift = 0, gmacro_dim[3] = {0, 0, 0}, gmacro_words = 0;
+  // per scene object its cell range (ix_min, iy_min, iz_min, ix_max, iy_max, iz_max), from the cell lists
+  std::vector<int32_t> grid_cells;
+  // the Grid scene's shadow tree (drt_upload_grid_shadow_bvh, triangle scenes): 4-ary records with
+  // widened child boxes, the primitives in its BVH's order, per such primitive its cell range (32-B
+  // LeafBoxRecord-shaped records read by the certificate), its big-leaf table
+  bool has_gv = false;
+  DevBuf d_gv_wnodes, d_gv_range, d_gv_prims, d_gv_big;
+  uint32_t gv_wroot = 0;
   // frame scratch
   DevBuf d_frame, d_rays, d_out, d_counter;
   // frame scratch per slot (drt_frame_params.slot): frames on different slots may be in flight
@@ -135,6 +145,7 @@ struct drt_ctx {
   // wavefront replay (WfArgs): shadow queries, their Phong factors and answers, per-level records
   DevBuf d_wf_rays_s[DRT_FRAME_SLOTS], d_wf_nl_s[DRT_FRAME_SLOTS], d_wf_occ_s[DRT_FRAME_SLOTS], d_wf_lvl_s[DRT_FRAME_SLOTS];
   DevBuf d_wf_cnt_s[DRT_FRAME_SLOTS];  // compact queries: per (band, level, 64-slot group) the group's query count
+  DevBuf d_wf_fb_s[DRT_FRAME_SLOTS];   // the Grid shadow tree's undecided queries (TraceArgs::fb_list)
   int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
@@ -314,8 +325,9 @@ static bool wide_tree_valid(const drt_bvh_node* nodes, uint32_t n_nodes, uint32_
 // wide node's children are its binary node's two children, the inner one with the largest box
 // surface replaced by its two children until there are four (or only leaves).  Records in depth-
 // first order.  False if a record cannot be quantised or 3 * depth would overflow the shadow stack.
+// widen > 0 (the Grid scene's tree, drt_upload_grid_shadow_bvh): every child box grown by widen on each side.
 static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& leaf_descs,
-                       std::vector<WideNodeRecord>& out, uint32_t& root) {
+                       std::vector<WideNodeRecord>& out, uint32_t& root, double widen = 0.0) {
   out.clear();
   if (nodes[0].leaf) return false;
   auto area = [&](uint32_t i) {
@@ -365,8 +377,8 @@ static bool build_wide(const drt_bvh_node* nodes, const std::vector<uint32_t>& l
     for (int a = 0; a < 3; a++) {
       double lo[kWideK], hi[kWideK];
       for (int k = 0; k < n; k++) {
-        lo[k] = nodes[ch[k]].bmin[a];
-        hi[k] = nodes[ch[k]].bmax[a];
+        lo[k] = (double)nodes[ch[k]].bmin[a] - widen;
+        hi[k] = (double)nodes[ch[k]].bmax[a] + widen;
       }
       uint32_t e = 0;
       if (!quantize_axis(lo, hi, n, r.p[a], e, r.q + kWideW * (2 * a), r.q + kWideW * (2 * a + 1))) return false;
@@ -463,7 +475,7 @@ int drt_upload_scene(drt_ctx* c, const drt_scene_desc* s) {
   if (!c || !s) return DRT_E_INVALID;
   // Nothing renders against a half-replaced scene: the context's scene and accelerator are
   // invalid from here until this upload has committed every buffer.
-  c->has_scene = c->has_bvh = c->has_grid = false;
+  c->has_scene = c->has_bvh = c->has_grid = c->has_gv = false;
   if (s->camera.res_x <= 0 || s->camera.res_y <= 0) DRT_FAIL(c, DRT_E_INVALID, "camera resolution must be positive");
   if (s->n_prims < 0 || (s->n_prims > 0 && !s->prims)) DRT_FAIL(c, DRT_E_INVALID, "bad primitive array");
   if (s->n_lights < 0 || (s->n_lights > 0 && !s->lights)) DRT_FAIL(c, DRT_E_INVALID, "bad light array");
@@ -544,7 +556,7 @@ int drt_set_camera(drt_ctx* c, const drt_camera* k) {
 int drt_upload_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, const uint32_t* order, uint32_t n_obj) {
   if (!c || !nodes || n_nodes == 0) return DRT_E_INVALID;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its BVH");
-  c->has_bvh = c->has_grid = false;  // until this upload commits
+  c->has_bvh = c->has_grid = c->has_gv = false;  // until this upload commits
   if ((int)n_obj != c->n_prims || (n_obj && !order)) DRT_FAIL(c, DRT_E_INVALID, "object_order must cover all %d objects", c->n_prims);
   std::vector<uint8_t> seen(n_obj, 0);
   for (uint32_t i = 0; i < n_obj; i++) {
@@ -720,7 +732,7 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
                     const int32_t* co, int64_t n_refs) {
   if (!c || !dims || !bmin || !bmax || !cs || (n_refs > 0 && !co)) return DRT_E_INVALID;
   if (!c->has_scene) DRT_FAIL(c, DRT_E_STATE, "upload the scene before its grid");
-  c->has_bvh = c->has_grid = false;  // until this upload commits
+  c->has_bvh = c->has_grid = c->has_gv = false;  // until this upload commits
   // A scene without objects: Grid::Build's widths overflow (float FLT_MAX - -FLT_MAX), the cell
   // counts come out NaN -> INT_MIN and the grid has no cells (grid.cpp:56-67); its box is
   // inverted, so every ray misses it.  Same here with one empty cell under that box.
@@ -742,6 +754,24 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
     if (co[i] < 0 || co[i] >= c->n_prims) DRT_FAIL(c, DRT_E_INVALID, "bad cell object");
     o32[i] = (uint32_t)co[i];
   }
+  // every object's cell range: Grid::Build registers an object in every cell of its box's range
+  // (grid.cpp:78-92), so the range is the min / max over the cells that list it
+  std::vector<int32_t> cells_of((size_t)c->n_prims * 6);
+  for (int i = 0; i < c->n_prims; i++) {
+    int32_t* r = &cells_of[(size_t)i * 6];
+    r[0] = r[1] = r[2] = INT32_MAX;
+    r[3] = r[4] = r[5] = -1;
+  }
+  for (int z = 0; z < dims[2]; z++)
+    for (int y = 0; y < dims[1]; y++)
+      for (int x = 0; x < dims[0]; x++) {
+        const size_t ci = (size_t)x + (size_t)dims[0] * y + (size_t)dims[0] * dims[1] * z;
+        for (uint32_t k = s32[ci]; k < s32[ci + 1]; k++) {
+          int32_t* r = &cells_of[(size_t)o32[k] * 6];
+          r[0] = std::min(r[0], x); r[1] = std::min(r[1], y); r[2] = std::min(r[2], z);
+          r[3] = std::max(r[3], x); r[4] = std::max(r[4], y); r[5] = std::max(r[5], z);
+        }
+      }
   DRT_HIP(c, hipSetDevice(c->device));
   DRT_HIP(c, c->d_cell_start.ensure(4 * s32.size()));
   DRT_HIP(c, hipMemcpy(c->d_cell_start.p, s32.data(), 4 * s32.size(), hipMemcpyHostToDevice));
@@ -873,8 +903,81 @@ int drt_upload_grid(drt_ctx* c, const int32_t dims[3], const float bmin[3], cons
   memcpy(c->gdim, dims, sizeof(c->gdim));
   memcpy(c->gmin, bmin, sizeof(c->gmin));
   memcpy(c->gmax, bmax, sizeof(c->gmax));
+  c->grid_cells = std::move(cells_of);
   c->has_grid = true;
   c->has_bvh = false;
+  return DRT_OK;
+}
+
+int drt_upload_grid_shadow_bvh(drt_ctx* c, const drt_bvh_node* nodes, uint32_t n_nodes, const uint32_t* order,
+                               uint32_t n_obj) {
+  if (!c || !nodes || n_nodes == 0) return DRT_E_INVALID;
+  if (!c->has_grid) DRT_FAIL(c, DRT_E_STATE, "upload the grid before its shadow tree");
+  c->has_gv = false;  // until this upload commits
+  if ((int)n_obj != c->n_prims || (n_obj && !order)) DRT_FAIL(c, DRT_E_INVALID, "object_order must cover all %d objects", c->n_prims);
+  if (!c->tri_only) DRT_FAIL(c, DRT_E_UNSUPPORTED, "the Grid's shadow tree serves triangle scenes");
+  if (n_obj > kFirstMask) DRT_FAIL(c, DRT_E_UNSUPPORTED, "more than %u objects", kFirstMask);
+  std::vector<uint8_t> seen(n_obj, 0);
+  for (uint32_t i = 0; i < n_obj; i++) {
+    if (order[i] >= n_obj || seen[order[i]]) DRT_FAIL(c, DRT_E_INVALID, "object_order is not a permutation");
+    seen[order[i]] = 1;
+  }
+  for (uint32_t i = 0; i < n_nodes; i++) {
+    const drt_bvh_node& nd = nodes[i];
+    if (nd.leaf ? (uint64_t)nd.index + nd.n_objs > n_obj : ((uint64_t)nd.index + 1 >= n_nodes || nd.index <= i))
+      DRT_FAIL(c, DRT_E_INVALID, "node %u out of range", i);
+  }
+  if (!wide_tree_valid(nodes, n_nodes, n_obj)) DRT_FAIL(c, DRT_E_INVALID, "not a tree of nested boxes over every object");
+  // leaf descriptors (oversized leaves through the big-leaf table, as drt_upload_bvh)
+  std::vector<uint2> big;
+  std::vector<uint32_t> dsc(n_nodes, 0u);
+  for (uint32_t i = 0; i < n_nodes; i++) {
+    const drt_bvh_node& nd = nodes[i];
+    if (!nd.leaf) continue;
+    if (nd.n_objs < kBigLeaf) {
+      dsc[i] = leaf_desc(nd.index, nd.n_objs);
+    } else {
+      big.push_back(make_uint2(nd.index, nd.n_objs));
+      dsc[i] = leaf_desc((uint32_t)big.size() - 1, kBigLeaf);
+    }
+  }
+  // Child boxes grown by 2^-16 of the scene's largest coordinate: every primitive whose test reports a
+  // hit at t < range lies inside its grown box (the test's and the slab arithmetic's float errors are a
+  // few 2^-24 of the coordinates), so the walk is an any-hit over every object and a query it finds no
+  // hit for is one Grid::Traverse(Ray&) finds none for either.
+  double m = 0.0;
+  for (int a = 0; a < 3; a++) m = std::max(m, std::max(std::fabs((double)nodes[0].bmin[a]), std::fabs((double)nodes[0].bmax[a])));
+  const double widen = std::ldexp(m, -16);
+  std::vector<WideNodeRecord> wide;
+  uint32_t wroot = 0;
+  if (!build_wide(nodes, dsc, wide, wroot, widen)) DRT_FAIL(c, DRT_E_UNSUPPORTED, "no shadow tree for this grid scene");
+  // primitives in the tree's order, and per such primitive its cell range (grid_certificate)
+  std::vector<PrimRecord> perm(n_obj);
+  std::vector<LeafBoxRecord> rng((size_t)n_obj + 2, LeafBoxRecord{});  // + 2: the node step's tail slot reads
+  const bool nocert = env_int("DRT_GRID_TREE_NOCERT", 0) != 0;  // (tests) every hit to the Grid walk
+  for (uint32_t i = 0; i < n_obj; i++) {
+    perm[i] = c->prims_scene[order[i]];
+    const int32_t* r = &c->grid_cells[(size_t)order[i] * 6];
+    LeafBoxRecord& b = rng[i];
+    if (r[3] < 0 || nocert) {  // listed in no cell: an inverted range, never certified
+      b.box[0] = b.box[1] = b.box[2] = 1.0f;
+      b.box[3] = b.box[4] = b.box[5] = 0.0f;
+    } else {
+      for (int k = 0; k < 6; k++) b.box[k] = (float)r[k];
+    }
+  }
+  DRT_HIP(c, hipSetDevice(c->device));
+  DRT_HIP(c, c->d_gv_wnodes.ensure(sizeof(WideNodeRecord) * wide.size()));
+  DRT_HIP(c, hipMemcpy(c->d_gv_wnodes.p, wide.data(), sizeof(WideNodeRecord) * wide.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_gv_range.ensure(sizeof(LeafBoxRecord) * rng.size()));
+  DRT_HIP(c, hipMemcpy(c->d_gv_range.p, rng.data(), sizeof(LeafBoxRecord) * rng.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_gv_prims.ensure(sizeof(PrimRecord) * perm.size() + kPrimPadBytes));
+  DRT_HIP(c, hipMemset(c->d_gv_prims.p, 0, sizeof(PrimRecord) * perm.size() + kPrimPadBytes));
+  DRT_HIP(c, hipMemcpy(c->d_gv_prims.p, perm.data(), sizeof(PrimRecord) * perm.size(), hipMemcpyHostToDevice));
+  DRT_HIP(c, c->d_gv_big.ensure(sizeof(uint2) * std::max<size_t>(1, big.size())));
+  if (!big.empty()) DRT_HIP(c, hipMemcpy(c->d_gv_big.p, big.data(), sizeof(uint2) * big.size(), hipMemcpyHostToDevice));
+  c->gv_wroot = wroot;
+  c->has_gv = true;
   return DRT_OK;
 }
 
@@ -1348,7 +1451,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
           c->d_wf_nl_s[slot].fit(sizeof(float2) * std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_occ_s[slot].fit(std::max<uint64_t>(q, 1)) == hipSuccess &&
           c->d_wf_lvl_s[slot].fit(sizeof(float4) * levels * P.wf_chunk) == hipSuccess &&
-          (!compact || c->d_wf_cnt_s[slot].fit(cnt_bytes) == hipSuccess)) {
+          (!compact || c->d_wf_cnt_s[slot].fit(cnt_bytes) == hipSuccess) &&
+          (!(compact && c->accel == DRT_ACCEL_GRID && c->has_gv) ||
+           c->d_wf_fb_s[slot].fit(sizeof(uint32_t) * std::max<uint64_t>(q, 1)) == hipSuccess)) {
         wavefront = true;
         W.rays = c->d_wf_rays_s[slot].as<float4>();
         W.rays_b = W.rays + std::max<uint64_t>(q, 1);
@@ -1364,7 +1469,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
       } else {
         (void)hipGetLastError();
         for (DevBuf* b : {&c->d_wf_rays_s[slot], &c->d_wf_nl_s[slot], &c->d_wf_occ_s[slot], &c->d_wf_lvl_s[slot],
-                          &c->d_wf_cnt_s[slot]})
+                          &c->d_wf_cnt_s[slot], &c->d_wf_fb_s[slot]})
           b->release();
       }
     }
@@ -1465,7 +1570,25 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
         A.band = W.band;
         A.parts = W.bands;
         A.part_len = W.bands == 8 ? part_len : (uint32_t)q;
-        launch_grid_stream(S, A, c->tri_only, stats, env_int("DRT_WAVEFRONT_GRID_WAVES", 7), F2.grid_walk, F2.grid_pairs, st);
+        // (round 6) the Grid scene's shadow tree answers the queries it can certify, the Grid walk the rest
+        // (trace_stream GV + grid_fallback).  Stats frames keep the walk, so that their work
+        // counters stay the reference's cell / object counts (DRT_GRID_SHADOW_TREE=2: the tree there too,
+        // its work in the wide_* counters); DRT_GRID_SHADOW_TREE=0: the walk for every frame.
+        const int gv = env_int("DRT_GRID_SHADOW_TREE", 1);
+        if (c->has_gv && c->tri_only && c->d_wf_fb_s[slot].p && (gv >= 2 || (gv == 1 && !stats))) {
+          SceneArgs ST = S;
+          ST.prims = c->d_gv_prims.as<float4>();
+          ST.wnodes = c->d_gv_wnodes.as<float4>();
+          ST.wleaf = c->d_gv_range.as<float4>();
+          ST.wroot = c->gv_wroot;
+          ST.big_leaves = c->d_gv_big.as<uint2>();
+          A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 12);
+          A.fb_list = c->d_wf_fb_s[slot].as<uint32_t>();
+          A.fb_count = counter + 224;  // (zeroed with the chunk's claim counters)
+          launch_grid_tree_stream(ST, S, A, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);
+        } else {
+          launch_grid_stream(S, A, c->tri_only, stats, env_int("DRT_WAVEFRONT_GRID_WAVES", 7), F2.grid_walk, F2.grid_pairs, st);
+        }
         DRT_HIP(c, hipGetLastError());
       } else if (q && W.grid) {
         // the Grid's shadow queries on its persistent stepper (MODE_QSTREAM): Grid::Traverse(Ray&)'s answer

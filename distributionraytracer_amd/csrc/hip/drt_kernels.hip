@@ -801,7 +801,8 @@ enum LaneFlag : uint32_t {
   LF_RESUME = 512u, // MODE_SEQ tail: the lane took over a pixel; its next sample starts in finish_sample
   LF_LEAFCONT = 1024u, // BVH: `cur` is the rest of a leaf whose first primitives were tested (not a new visit)
   LF_WIDE = 2048u,     // BVH shadow query on the 4-ary shadow tree (drt_layout.hpp)
-  LF_VERIFY = 4096u    // shadow tree: primitive `cur` was hit within range; check its leaf's exact box
+  LF_VERIFY = 4096u,   // shadow tree: primitive `cur` was hit within range; check its leaf's exact box
+  LF_GVFB = 8192u      // Grid scene's shadow tree (trace_stream GV): no cell certificate, the Grid walk answers
 };
 
 struct Lane {
@@ -875,6 +876,54 @@ __device__ __forceinline__ bool wide_ray_ok(const RayP& r) {
   const float mo = fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
   return mi <= 0x1p40f && mo <= 0x1p60f;  // false for NaN
 #endif
+}
+
+// Grid::Traverse(Ray&)'s first step (grid.cpp:318-324): a shadow ray whose slab test misses the grid box
+// counts as shadowed.  The same float arithmetic as grid_traverse / grid_init.
+__device__ __forceinline__ bool grid_box_missed(const SceneArgs& S, const RayP& r) {
+  const float x0 = S.gmin[0], y0 = S.gmin[1], z0 = S.gmin[2], x1 = S.gmax[0], y1 = S.gmax[1], z1 = S.gmax[2];
+  float txmin, tymin, tzmin, txmax, tymax, tzmax;
+  if (r.sx()) { txmin = (x0 - r.o.x) * r.ix; txmax = (x1 - r.o.x) * r.ix; } else { txmin = (x1 - r.o.x) * r.ix; txmax = (x0 - r.o.x) * r.ix; }
+  if (r.sy()) { tymin = (y0 - r.o.y) * r.iy; tymax = (y1 - r.o.y) * r.iy; } else { tymin = (y1 - r.o.y) * r.iy; tymax = (y0 - r.o.y) * r.iy; }
+  if (r.sz()) { tzmin = (z0 - r.o.z) * r.iz; tzmax = (z1 - r.o.z) * r.iz; } else { tzmin = (z1 - r.o.z) * r.iz; tzmax = (z0 - r.o.z) * r.iz; }
+  float t0 = (txmin > tymin) ? txmin : tymin;
+  if (tzmin > t0) t0 = tzmin;
+  float t1 = (txmax < tymax) ? txmax : tymax;
+  if (tzmax < t1) t1 = tzmax;
+  return t0 > t1 || t1 < 0.0f;  // grid.cpp:170 (NaN compares false: not missed, as there)
+}
+
+// The Grid cell certificate of a shadow-tree hit (trace_stream GV).  Primitive P was hit at t < range.
+// Grid::Traverse(Ray&) (grid.cpp:309-358) tests P as soon as its DDA enters any cell of P's cell range
+// (Grid::Build registers P in every cell of [min, max] of its box, grid.cpp:78-92), and the walk
+// covers the ray from its start to the grid's exit.  The ray's point at t, p = o + t d (in double), lies
+// in the grid; if it lies in a cell c of P's range, more than `margin` of a cell from each of c's faces,
+// the DDA visits c — its face crossing times are the float-rounded Init_Traverse values stepped in
+// double, off by less than 16 eps K n cells after n steps (|t_min|, |dt| and the products each carry a
+// few float roundings of values up to K grid widths, K = 1 + max_a (|min_a| + |max_a|) / width_a), and
+// the walk's start cell is off only within that distance of a face — so the walk tests P there and
+// answers occluded (or finds another occluder first).  margin = 128 eps K n_max, 8x that bound.
+// rng0 = (ix_min, iy_min, iz_min, ix_max), rng1 = (iy_max, iz_max, ., .) as floats.
+__device__ __forceinline__ bool grid_certificate(const SceneArgs& S, const RayP& r, float t, const float4& rng0,
+                                                 const float4& rng1) {
+  const int nm = max(S.gdim[0], max(S.gdim[1], S.gdim[2]));
+  double K = 1.0;
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+    K = fmax(K, 1.0 + (fabs((double)S.gmin[a]) + fabs((double)S.gmax[a])) / ((double)S.gmax[a] - (double)S.gmin[a]));
+  const double margin = 128.0 * 0x1p-23 * K * (double)nm;
+  const double td = (double)t;
+  bool ok = margin < 0.25;  // (false for NaN: a degenerate grid leaves every query to the walk)
+  const float lo[3] = {rng0.x, rng0.y, rng0.z}, hi[3] = {rng0.w, rng1.x, rng1.y};
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const double p = (double)o[a] + td * (double)d[a];
+    const double u = (p - (double)S.gmin[a]) * (double)S.gdim[a] / ((double)S.gmax[a] - (double)S.gmin[a]);
+    const double c = floor(u), f = u - c;
+    ok = ok && f > margin && f < 1.0 - margin && c >= (double)lo[a] && c <= (double)hi[a];
+  }
+  return ok;  // (false for NaN)
 }
 
 // Grid::Init_Traverse (grid.cpp:160-245) for the lane's query: grid-box entry, first cell and
@@ -1205,8 +1254,14 @@ __device__ __forceinline__ uint64_t stamp_cycles() {
 // lane's — a wave's queries come from consecutive samples of one pixel toward one light point, so their
 // walks coincide for long stretches — those lanes read it through one scalar load (the scalar cache)
 // instead of per-lane vector loads on the vector-memory path the kernel is bound by.
+// GV (round 6, the Grid scene's shadow queries on a shadow tree; trace_stream GV): the tree is
+// collapsed from a BVH of the Grid scene's objects with every child box widened (drt_upload_grid_shadow_bvh),
+// a primitive hit counts when t < range (grid.cpp:340), and instead of the leaf's box the hit is checked
+// against the Grid: the ray's point at that t must lie inside a cell of the primitive's cell range,
+// away from every cell face by more than the DDA's rounding (grid_certificate).  A certified hit is
+// one Grid::Traverse(Ray&) would find; an uncertified one leaves the query to the Grid walk (LF_GVFB).
 template <bool TRI_ONLY, bool STATS, int CAP, int KIND = 0, int LEAF1 = 1, bool WIDE = false, bool UNI = false,
-          class LaneT>
+          bool GV = false, class LaneT>
 __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte* lds, uint32_t* ov_desc,
                                           float* ov_t, bool wave_finite, Counters& C, uint64_t& cyc_leaf) {
   constexpr uint32_t kLdsBytes = (uint32_t)CAP * kRowBytes;  // desc part; the t part follows
@@ -1424,10 +1479,15 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
   }
   if (WIDE && verify) {  // the exact reference leaf box of primitive `cur`, hit within range
     if (STATS) C.v[ST_W_VERIFY]++;
-    float tv;
-    const bool in = box_test_finite(s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, L.q, tv);
     fl &= ~LF_VERIFY;
-    fl = in ? ((fl | LF_HIT) & ~LF_TRAV) : (fl | LF_POP);
+    if constexpr (GV) {  // s0, s1: the primitive's cell range (grid_certificate)
+      const bool in = grid_certificate(S, L.q, L.best_t, s0, s1);
+      fl = (fl | (in ? LF_HIT : LF_GVFB)) & ~LF_TRAV;
+    } else {
+      float tv;
+      const bool in = box_test_finite(s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, L.q, tv);
+      fl = in ? ((fl | LF_HIT) & ~LF_TRAV) : (fl | LF_POP);
+    }
   }
   if (inner && !wide) {
     if (STATS) C.v[shadow ? ST_S_INNER : ST_C_INNER]++;
@@ -1484,11 +1544,13 @@ __device__ __forceinline__ void node_step(const SceneArgs& S, LaneT& L, LdsByte*
       float t;
       if (hit_prim_rec<TRI_ONLY>(p0, p1, p2, L.q, t)) {
         if (shadow) {
-          if (t <= L.thr) {
+          if (GV ? t < L.thr : t <= L.thr) {
             // shadow tree: the leaf was entered through a containing box; its exact box decides
+            // (GV: the Grid cell certificate, at this t)
             if (wide) {
               fl |= LF_VERIFY;
               L.cur = prim;
+              if (GV) L.best_t = t;
             } else {
               fl = (fl | LF_HIT) & ~LF_TRAV;
             }
@@ -2618,7 +2680,11 @@ struct TLane {
   float best_t, thr;
 };
 
-template <bool TRI_ONLY, int KIND, int WAVES, bool STATS>
+// GV (round 6): the Grid scene's wavefront shadow queries on its shadow tree (node_step GV; S carries the
+// Grid and, in its BVH fields, the tree): a ray that misses the grid box is occluded (grid.cpp:323), a
+// certified hit is occluded, no hit is not, and the rest (no certificate, or a ray the tree does not
+// take) go to A.fb_list for grid_fallback, which walks the Grid.
+template <bool TRI_ONLY, int KIND, int WAVES, bool STATS, bool GV = false>
 __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, TraceArgs A) {
   constexpr int CAP = lds_cap(WAVES);
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_bytes[];
@@ -2698,16 +2764,28 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
           L.best_prim = 0xFFFFFFFFu;
           L.spa &= kRowBytes - 1u;
           L.cur = S.root_desc;
+          const bool fin = ray_finite(L.q);
+          if constexpr (GV) {
+            L.best_prim = (uint32_t)at;  // (the query's position, for grid_fallback)
+            const bool wok = fin && wide_ray_ok(L.q);
+            const bool missed = grid_box_missed(S, L.q);
+            L.fl = LF_SHADOW | LF_FINITE | (missed ? LF_HIT : (wok ? (LF_TRAV | LF_WIDE) : LF_GVFB));
+            L.cur = S.wroot;
+            if (STATS) {
+              C.v[ST_SHADOW]++;
+              if (!missed && wok) C.v[ST_W_RAYS]++;
+            }
+          } else {
           float tmp;
           const bool root = box_hit(S.root_box[0], S.root_box[1], S.root_box[2], S.root_box[3], S.root_box[4],
                                     S.root_box[5], L.q, tmp);  // bvh.cpp:242 / :328
-          const bool fin = ray_finite(L.q);
           L.fl = (KIND == 2 ? LF_SHADOW : 0u) | (root ? LF_TRAV : 0u) | (fin ? LF_FINITE : 0u);
           if (STATS) C.v[KIND == 2 ? ST_SHADOW : ST_CLOSEST]++;
           if (KIND == 2 && fin && S.wnodes != nullptr && wide_ray_ok(L.q)) {  // finite shadow rays: the 4-ary shadow tree
             if (STATS) C.v[ST_W_RAYS]++;
             L.fl |= LF_WIDE;
             L.cur = S.wroot;
+          }
           }
           }
         }
@@ -2727,12 +2805,14 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
       // one primitive of a leaf per step in triangle scenes only, as in the path kernel (mixed-primitive
       // scenes measured ~10 % slower with it there)
       if (in_trav)
-        node_step<TRI_ONLY, STATS, CAP, KIND, TRI_ONLY ? 1 : 0, KIND == 2, kUniFetch && KIND == 2>(
+        node_step<TRI_ONLY, STATS, CAP, KIND, TRI_ONLY ? 1 : 0, KIND == 2, kUniFetch && KIND == 2 && !GV, GV>(
             S, L, (LdsByte*)lds_bytes, ov_desc, ov_t,
                                                                             wave_finite, C, cyc_leaf);
     }
     if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
-      if (KIND == 2) {
+      if (GV && (L.fl & LF_GVFB)) {  // the Grid walk answers it (grid_fallback)
+        A.fb_list[atomicAdd(A.fb_count, 1u)] = L.best_prim;
+      } else if (KIND == 2) {
         wf_st(&A.occ_out[L.item], (uint8_t)((L.fl & LF_HIT) ? 1 : 0));
       } else {
         const bool hit = (L.fl & LF_HIT) != 0u;
@@ -2833,6 +2913,24 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
       for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
       if (lane == 0 && v) atomicAdd(&A.stats[s], v);
     }
+  }
+}
+
+// The Grid scene's shadow queries that the shadow tree left undecided (trace_stream GV): each on
+// Grid::Traverse(Ray&) (grid.cpp:309-358, grid_traverse), one per thread over the list trace_stream
+// appended (A.fb_list: the queries' positions in the compact array, *A.fb_count of them).
+template <bool TRI_ONLY>
+__global__ void __launch_bounds__(256) grid_fallback(SceneArgs S, TraceArgs A) {
+  Counters C;
+  const uint32_t n = *A.fb_count;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const uint32_t at = A.fb_list[i];
+    const float4 a = A.rays[at], b = A.rays_b[at];
+    const RayP r = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
+    float t;
+    uint32_t prim;
+    const bool occ = grid_traverse<TRI_ONLY, false>(S, r, true, a.w, t, prim, C);
+    A.occ_out[__float_as_uint(b.w)] = occ ? 1 : 0;
   }
 }
 
@@ -3281,7 +3379,7 @@ void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, in
                      n_tiles, n_shards, tiles_per_shard, res_x, res_y);
 }
 
-template <bool T, int K, int W, bool ST>
+template <bool T, int K, int W, bool ST, bool GV = false>
 static void launch_stream_w(const SceneArgs& S, const TraceArgs& A, hipStream_t st) {
   const size_t lds = (size_t)lds_cap(W) * kPBlock * 8;
   static int grid = 0;  // resident blocks across the device (per instantiation)
@@ -3289,12 +3387,28 @@ static void launch_stream_w(const SceneArgs& S, const TraceArgs& A, hipStream_t 
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_stream<T, K, W, ST>, kPBlock, lds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)trace_stream<T, K, W, ST, GV>, kPBlock, lds);
     grid = std::max(1, cus) * std::max(1, per_cu);
   }
   const uint64_t need = ((uint64_t)A.n + kPBlock - 1) / kPBlock;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)grid));
-  hipLaunchKernelGGL((trace_stream<T, K, W, ST>), dim3(blocks), dim3(kPBlock), lds, st, S, A);
+  hipLaunchKernelGGL((trace_stream<T, K, W, ST, GV>), dim3(blocks), dim3(kPBlock), lds, st, S, A);
+}
+// the Grid scene's compact wavefront shadow queries on its shadow tree (trace_stream GV, triangle scenes),
+// then grid_fallback on the Grid for the undecided ones (SG: the Grid's own SceneArgs, scene-order records)
+void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const TraceArgs& A, bool stats, int waves,
+                             hipStream_t st) {
+  if (stats) launch_stream_w<true, 2, 7, true, true>(ST_, A, st);
+  else if (waves <= 6) launch_stream_w<true, 2, 6, false, true>(ST_, A, st);
+  else launch_stream_w<true, 2, 7, false, true>(ST_, A, st);
+  static int blocks = 0;
+  if (!blocks) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    blocks = std::max(1, cus) * 8;
+  }
+  hipLaunchKernelGGL((grid_fallback<true>), dim3(blocks), dim3(256), 0, st, SG, A);
 }
 template <bool T, int K, bool ST>
 static void launch_stream_k(const SceneArgs& S, const TraceArgs& A, int waves, hipStream_t st) {

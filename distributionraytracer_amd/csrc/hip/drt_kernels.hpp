@@ -249,6 +249,10 @@ struct TraceArgs {
   // starts on the range of its XCD and moves on when that one is claimed (parts 1: one counter)
   int parts;
   uint32_t part_len;
+  // the Grid scene's shadow tree (trace_stream GV): queries it leaves to the Grid walk, by their position
+  // in the query array, and their count (grid_fallback)
+  uint32_t* fb_list;
+  unsigned int* fb_count;
 };
 
 struct ReduceArgs {

@@ -1,5 +1,7 @@
 // drt_host_capi.cpp — C entry points (include/drt_host.h) over the C++ host scene API.
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../../include/drt_host.h"
 #include "../../../include/drt_scene.hpp"
@@ -10,6 +12,9 @@ struct drt_scene {
   Scene scene;
   BVH bvh;
   Grid grid;
+  // a triangle Grid scene's BVH for its shadow tree (drt_upload_grid_shadow_bvh; DRT_GRID_SHADOW_TREE=0: none)
+  BVH gv_bvh;
+  bool has_gv_bvh = false;
   Material* current = nullptr;
   bool built = false;
 };
@@ -140,6 +145,16 @@ int drt_scene_build(drt_scene* s) {  // main.cpp:1023-1049
   } else if (s->scene.GetAccelStruct() == GRID_ACC) {
     s->grid = Grid();  // Grid::Build appends to the grid's object list (grid.cpp:45)
     s->grid.Build(objs);
+    // the Grid frame's shadow queries walk a tree of the same objects (triangle scenes, round 6)
+    const char* e = getenv("DRT_GRID_SHADOW_TREE");
+    bool tri = !objs.empty() && !(e && atoi(e) == 0);
+    for (Object* o : objs)
+      if (!dynamic_cast<Triangle*>(o)) { tri = false; break; }
+    s->gv_bvh = BVH();
+    s->has_gv_bvh = tri;
+    if (tri) s->gv_bvh.Build(objs);
+  } else {
+    s->has_gv_bvh = false;
   }
   s->built = true;
   return DRT_OK;
@@ -214,7 +229,24 @@ int drt_scene_upload(drt_ctx* ctx, drt_scene* s) {
   if (!s->scene.GetCamera()) return DRT_E_STATE;
   if (s->scene.GetSkyBoxFlg() && !s->scene.SkyboxComplete()) return DRT_E_STATE;
   if (!s->built) drt_scene_build(s);
-  return upload_scene(ctx, s->scene, &s->bvh, &s->grid);
+  const int rc = upload_scene(ctx, s->scene, &s->bvh, &s->grid);
+  if (rc || !s->has_gv_bvh || s->scene.GetAccelStruct() != GRID_ACC) return rc;
+  const auto& nd = s->gv_bvh.nodeList();
+  std::vector<drt_bvh_node> n(nd.size());
+  for (size_t i = 0; i < nd.size(); i++) {
+    const AABB& b = nd[i].bbox;
+    n[i].bmin[0] = b.min.x; n[i].bmin[1] = b.min.y; n[i].bmin[2] = b.min.z;
+    n[i].bmax[0] = b.max.x; n[i].bmax[1] = b.max.y; n[i].bmax[2] = b.max.z;
+    n[i].leaf = nd[i].leaf ? 1u : 0u;
+    n[i].index = nd[i].index;
+    n[i].n_objs = nd[i].leaf ? nd[i].n_objs : 0u;
+  }
+  const auto& ob = s->gv_bvh.objectOrder();
+  std::vector<uint32_t> ord(ob.size());
+  for (size_t i = 0; i < ob.size(); i++) ord[i] = (uint32_t)ob[i]->scene_index;
+  // without a tree the Grid walk answers every query: a tree the device cannot take is no error
+  const int g = drt_upload_grid_shadow_bvh(ctx, n.data(), (uint32_t)n.size(), ord.data(), (uint32_t)ord.size());
+  return g == DRT_E_UNSUPPORTED ? DRT_OK : g;
 }
 
 int drt_group_scene_upload(drt_group* g, drt_scene* s) {

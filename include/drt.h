@@ -199,6 +199,15 @@ int drt_upload_bvh(drt_ctx* ctx, const drt_bvh_node* nodes, uint32_t n_nodes, co
                    uint32_t n_objects);
 int drt_upload_grid(drt_ctx* ctx, const int32_t dims[3], const float bmin[3], const float bmax[3],
                     const int64_t* cell_start /* nx*ny*nz+1 */, const int32_t* cell_objs, int64_t n_refs);
+/* Optional, after drt_upload_grid of a triangle scene (round 6): a BVH of the same objects (the
+ * BVH::Build result, as drt_upload_bvh takes it).  The Grid frame's wavefront shadow queries then walk a
+ * 4-ary tree collapsed from it with widened boxes, and a hit counts only with a Grid cell certificate
+ * (the ray's point at the hit lies well inside a cell the object is listed in, so Grid::Traverse(Ray&),
+ * grid.cpp:309-358, finds it too); queries without one are walked on the Grid.  The answers are
+ * Grid::Traverse(Ray&)'s.  Any drt_upload_scene / drt_upload_grid / drt_upload_bvh drops it.
+ * DRT_GRID_SHADOW_TREE=0 keeps the Grid walk for every query. */
+int drt_upload_grid_shadow_bvh(drt_ctx* ctx, const drt_bvh_node* nodes, uint32_t n_nodes,
+                               const uint32_t* object_order, uint32_t n_objects);
 
 /* How a frame would run (no device work): work items (a (pixel, sample) pair, or a pixel whose
  * samples run in order), float4 sample slots, the frame mode (0 AA, 1 in-order keyed stream,
