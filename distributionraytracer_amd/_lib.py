@@ -54,7 +54,8 @@ class DrtFrameStats(C.Structure):
                                    "cycles_node", "cycles_shade", "stack_pushes", "stack_spills",
                                    "wave_leaf_iters", "cycles_leaf", "seq_pushed", "seq_popped")] + \
         [("seq_handover", C.c_int32), ("reserved", C.c_int32)] + \
-        [(n, C.c_uint64) for n in ("wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify")]
+        [(n, C.c_uint64) for n in ("wide_shadow_rays", "wide_inner", "wide_leaf", "wide_prims", "wide_verify",
+                                   "wide_grid_walks")]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if n.endswith("_ms") else int(getattr(self, n))) for n, _ in self._fields_

@@ -28,7 +28,7 @@ void launch_wf_gen(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipS
 void launch_grid_stream(const SceneArgs& S, const TraceArgs& A, bool tri_only, bool stats, int waves, int walk, int pairs,
                         hipStream_t st);
 void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const TraceArgs& A, bool stats, int waves,
-                             hipStream_t st);
+                             int walk, int pairs, unsigned int* fb_counter, hipStream_t st);
 void launch_wf_combine(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, hipStream_t st);
 void launch_wf_combine_reduce(const SceneArgs& S, const FrameArgs& F, const WfArgs& W, const ReduceArgs& R,
                               hipStream_t st);
@@ -1585,7 +1585,8 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
           A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 12);
           A.fb_list = c->d_wf_fb_s[slot].as<uint32_t>();
           A.fb_count = counter + 224;  // (zeroed with the chunk's claim counters)
-          launch_grid_tree_stream(ST, S, A, stats, env_int("DRT_WAVEFRONT_WAVES", 7), st);
+          launch_grid_tree_stream(ST, S, A, stats, env_int("DRT_WAVEFRONT_WAVES", 7), F2.grid_walk, F2.grid_pairs,
+                                  counter + 240, st);
         } else {
           launch_grid_stream(S, A, c->tri_only, stats, env_int("DRT_WAVEFRONT_GRID_WAVES", 7), F2.grid_walk, F2.grid_pairs, st);
         }
@@ -1861,6 +1862,7 @@ int drt_get_stats(drt_ctx* c, drt_frame_stats* out) {
       c->last.wide_leaf = s[ST_W_LEAF];
       c->last.wide_prims = s[ST_W_PRIMS];
       c->last.wide_verify = s[ST_W_VERIFY];
+      c->last.wide_grid_walks = s[ST_W_GRIDFB];
     }
     c->last.seq_handover = c->slot_handover[c->stats_slot] ? 1 : 0;
     if (c->last.seq_handover) {  // push / pop counts of the frame's continuation slots

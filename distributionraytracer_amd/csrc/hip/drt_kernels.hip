@@ -10,6 +10,7 @@
 //  * trace_kernel: batched BVH/Grid/NONE closest and shadow queries (the Traverse() API).
 //  * unshard_kernel: tile-compact shard buffers -> full frame.
 #include <algorithm>
+#include <cstdlib>
 
 #include "drt_device.hpp"
 #include "drt_kernels.hpp"
@@ -2812,6 +2813,7 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
     if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
       if (GV && (L.fl & LF_GVFB)) {  // the Grid walk answers it (grid_fallback)
         A.fb_list[atomicAdd(A.fb_count, 1u)] = L.best_prim;
+        if (STATS) C.v[ST_W_GRIDFB]++;
       } else if (KIND == 2) {
         wf_st(&A.occ_out[L.item], (uint8_t)((L.fl & LF_HIT) ? 1 : 0));
       } else {
@@ -2853,6 +2855,9 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t chunk_next = 0, chunk_end = 0, chunk_base = 0, chunk_cnt = 0;  // wave-uniform (as trace_stream)
   bool exhausted = false;
+  // A.fb_list (round 6): the queries the Grid scene's shadow tree left undecided (trace_stream GV), a
+  // dense list of *A.fb_count positions in the compact query array, claimed 256 at a time
+  const uint32_t fb_n = A.fb_list ? __builtin_amdgcn_readfirstlane(*(volatile const uint32_t*)A.fb_count) : A.n;
   uint32_t part = A.parts > 1 ? (__builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u) % (uint32_t)A.parts : 0u;
   uint32_t parts_done = 0;
   while (true) {
@@ -2860,13 +2865,15 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
     const int n_idle = __popcll(idle);
     if (n_idle >= A.refill_min || n_idle == 64) {
       while (chunk_next >= chunk_end && !exhausted) {  // claim 256 query slots of the wave's partition
-        const uint32_t pbeg = part * A.part_len, pend = min(pbeg + A.part_len, A.n);
+        const uint32_t pbeg = part * A.part_len, pend = min(pbeg + A.part_len, fb_n);
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(A.counter + 16u * part, kTraceChunk);
         base = __shfl(base, 0, 64) + pbeg;
         chunk_base = base;
         chunk_next = chunk_end = 0;
-        if (base < pend) {  // the chunk's four group counts (one row of the query array)
+        if (A.fb_list) {  // the shadow tree's undecided queries: a dense list of positions
+          chunk_end = base < pend ? min(base + kTraceChunk, pend) - base : 0u;
+        } else if (base < pend) {  // the chunk's four group counts (one row of the query array)
           const uint32_t row = base / A.band, o0 = base - row * A.band, bl = row / (uint32_t)A.pairs;
           chunk_cnt = *(const uint32_t*)(A.cnt + (size_t)bl * (A.band >> 6) + (o0 >> 6));
           chunk_end = (chunk_cnt & 0xffu) + ((chunk_cnt >> 8) & 0xffu) + ((chunk_cnt >> 16) & 0xffu) + (chunk_cnt >> 24);
@@ -2883,7 +2890,7 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
           const uint32_t p1 = chunk_cnt & 0xffu, p2 = p1 + ((chunk_cnt >> 8) & 0xffu), p3 = p2 + ((chunk_cnt >> 16) & 0xffu);
           const uint32_t j = (it >= p1 ? 1u : 0u) + (it >= p2 ? 1u : 0u) + (it >= p3 ? 1u : 0u);
           const uint32_t pre = j == 0u ? 0u : (j == 1u ? p1 : (j == 2u ? p2 : p3));
-          const size_t at = (size_t)(chunk_base + 64u * j + (it - pre));
+          const size_t at = A.fb_list ? (size_t)A.fb_list[chunk_base + it] : (size_t)(chunk_base + 64u * j + (it - pre));
           const float4 a = wf_ld(&A.rays[at]);
           const float4 b = wf_ld(&A.rays_b[at]);
           L.item = __float_as_uint(b.w);
@@ -3379,6 +3386,10 @@ void launch_unshard(const float* shards, float* frame, int tile, int tiles_x, in
                      n_tiles, n_shards, tiles_per_shard, res_x, res_y);
 }
 
+static bool env_fallback_kernel() {
+  const char* e = getenv("DRT_GRID_TREE_FALLBACK_THREADS");
+  return e && atoi(e) != 0;
+}
 template <bool T, int K, int W, bool ST, bool GV = false>
 static void launch_stream_w(const SceneArgs& S, const TraceArgs& A, hipStream_t st) {
   const size_t lds = (size_t)lds_cap(W) * kPBlock * 8;
@@ -3396,20 +3407,6 @@ static void launch_stream_w(const SceneArgs& S, const TraceArgs& A, hipStream_t 
 }
 // the Grid scene's compact wavefront shadow queries on its shadow tree (trace_stream GV, triangle scenes),
 // then grid_fallback on the Grid for the undecided ones (SG: the Grid's own SceneArgs, scene-order records)
-void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const TraceArgs& A, bool stats, int waves,
-                             hipStream_t st) {
-  if (stats) launch_stream_w<true, 2, 7, true, true>(ST_, A, st);
-  else if (waves <= 6) launch_stream_w<true, 2, 6, false, true>(ST_, A, st);
-  else launch_stream_w<true, 2, 7, false, true>(ST_, A, st);
-  static int blocks = 0;
-  if (!blocks) {
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    blocks = std::max(1, cus) * 8;
-  }
-  hipLaunchKernelGGL((grid_fallback<true>), dim3(blocks), dim3(256), 0, st, SG, A);
-}
 template <bool T, int K, bool ST>
 static void launch_stream_k(const SceneArgs& S, const TraceArgs& A, int waves, hipStream_t st) {
   if (waves >= 8) launch_stream_w<T, K, 8, ST>(S, A, st);
@@ -3430,6 +3427,33 @@ static void launch_grid_stream_w(const SceneArgs& S, const TraceArgs& A, int wal
   const uint64_t need = ((uint64_t)A.n + 255) / 256;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)grid));
   hipLaunchKernelGGL((grid_stream<T, W, ST>), dim3(blocks), dim3(256), lds, st, S, A, walk, pairs);
+}
+// (A.fb_list / fb_count; fb_counter: a zeroed claim counter for the second launch)
+void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const TraceArgs& A, bool stats, int waves,
+                             int walk, int pairs, unsigned int* fb_counter, hipStream_t st) {
+  if (stats) launch_stream_w<true, 2, 7, true, true>(ST_, A, st);
+  else if (waves <= 6) launch_stream_w<true, 2, 6, false, true>(ST_, A, st);
+  else launch_stream_w<true, 2, 7, false, true>(ST_, A, st);
+  if (env_fallback_kernel()) {  // (A/B) one query per thread, no refill
+    static int blocks = 0;
+    if (!blocks) {
+      int dev = 0, cus = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      blocks = std::max(1, cus) * 8;
+    }
+    hipLaunchKernelGGL((grid_fallback<true>), dim3(blocks), dim3(256), 0, st, SG, A);
+    return;
+  }
+  // grid_stream over the undecided queries' list: the persistent Grid stepper, refilled (its grid is
+  // sized for the whole query array; waves past the list's end retire at once)
+  TraceArgs B = A;
+  B.counter = fb_counter;
+  B.parts = 1;
+  B.part_len = A.n;
+  B.refill_min = 16;
+  if (stats) launch_grid_stream_w<true, 7, true>(SG, B, walk, pairs, st);
+  else launch_grid_stream_w<true, 7, false>(SG, B, walk, pairs, st);
 }
 // the Grid's compact wavefront shadow queries (grid_stream); waves per SIMD 5, 6 or 7
 void launch_grid_stream(const SceneArgs& S, const TraceArgs& A, bool tri_only, bool stats, int waves, int walk, int pairs,

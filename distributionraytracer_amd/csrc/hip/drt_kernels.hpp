@@ -55,7 +55,7 @@ enum StatSlot : int {
   // shadow queries on the 4-ary shadow tree (drt_layout.hpp): queries, inner-node visits, leaf
   // visits, primitive tests and exact leaf-box checks of in-range hits (the ST_S_* slots then
   // count only the shadow queries that walked the reference's binary tree)
-  ST_W_RAYS, ST_W_INNER, ST_W_LEAF, ST_W_PRIMS, ST_W_VERIFY,
+  ST_W_RAYS, ST_W_INNER, ST_W_LEAF, ST_W_PRIMS, ST_W_VERIFY, ST_W_GRIDFB,
   ST_COUNT
 };
 

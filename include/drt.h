@@ -182,6 +182,8 @@ typedef struct {
    * shadow_inner / shadow_leaf / shadow_prims then count only the queries (non-finite rays)
    * that walked the reference's binary tree. */
   uint64_t wide_shadow_rays, wide_inner, wide_leaf, wide_prims, wide_verify;
+  /* a Grid scene's shadow tree (drt_upload_grid_shadow_bvh): its queries left to the Grid walk */
+  uint64_t wide_grid_walks;
 } drt_frame_stats;
 
 int drt_create(drt_ctx** out, const drt_options* opt);
