@@ -3452,8 +3452,8 @@ void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const Tr
   B.parts = 1;
   B.part_len = A.n;
   B.refill_min = 16;
-  if (stats) launch_grid_stream_w<true, 7, true>(SG, B, walk, pairs, st);
-  else launch_grid_stream_w<true, 7, false>(SG, B, walk, pairs, st);
+  // (a stats frame counts each query once, in trace_stream: wide_grid_walks of them walked here)
+  launch_grid_stream_w<true, 7, false>(SG, B, walk, pairs, st);
 }
 // the Grid's compact wavefront shadow queries (grid_stream); waves per SIMD 5, 6 or 7
 void launch_grid_stream(const SceneArgs& S, const TraceArgs& A, bool tri_only, bool stats, int waves, int walk, int pairs,
