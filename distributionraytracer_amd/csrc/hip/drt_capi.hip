@@ -145,7 +145,7 @@ struct drt_ctx {
   // wavefront replay (WfArgs): shadow queries, their Phong factors and answers, per-level records
   DevBuf d_wf_rays_s[DRT_FRAME_SLOTS], d_wf_nl_s[DRT_FRAME_SLOTS], d_wf_occ_s[DRT_FRAME_SLOTS], d_wf_lvl_s[DRT_FRAME_SLOTS];
   DevBuf d_wf_cnt_s[DRT_FRAME_SLOTS];  // compact queries: per (band, level, 64-slot group) the group's query count
-  DevBuf d_wf_fb_s[DRT_FRAME_SLOTS];   // the Grid shadow tree's undecided queries (TraceArgs::fb_list)
+  DevBuf d_wf_fb_s[DRT_FRAME_SLOTS];   // the Grid shadow tree's undecided queries (TraceArgs::fb_rays)
   int cus = 0;  // compute units of the device (sizes the continuation slots)
   int stats_slot = 0;  // slot of the last frame (drt_get_stats reads its counters)
   drt_frame_stats last{};
@@ -1019,6 +1019,17 @@ static int scene_args(drt_ctx* c, int accel, SceneArgs& S, bool reference_order)
     memcpy(S.gdim, c->gdim, sizeof(S.gdim));
     memcpy(S.gmin, c->gmin, sizeof(S.gmin));
     memcpy(S.gmax, c->gmax, sizeof(S.gmax));
+    // the shadow tree's cell certificate (grid_certificate): n / width per axis, and 128 eps K n_max
+    double K = 1.0;
+    int nm = 1;
+    for (int a = 0; a < 3; a++) {
+      const double w = (double)c->gmax[a] - (double)c->gmin[a];
+      S.gscale[a] = (float)((double)c->gdim[a] / w);
+      K = std::max(K, 1.0 + (std::fabs((double)c->gmin[a]) + std::fabs((double)c->gmax[a])) / w);
+      nm = std::max(nm, c->gdim[a]);
+    }
+    const double margin = 128.0 * std::ldexp(1.0, -23) * K * nm;
+    S.gmargin = margin < 0.25 ? (float)margin : 1.0f;  // (1: no certificate, every hit to the Grid walk)
     S.cell_start = c->d_cell_start.as<uint32_t>();
     S.gmacro = c->d_macro.as<uint32_t>();
     S.cell_recs = c->d_cell_recs.as<float4>();
@@ -1453,7 +1464,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
           c->d_wf_lvl_s[slot].fit(sizeof(float4) * levels * P.wf_chunk) == hipSuccess &&
           (!compact || c->d_wf_cnt_s[slot].fit(cnt_bytes) == hipSuccess) &&
           (!(compact && c->accel == DRT_ACCEL_GRID && c->has_gv) ||
-           c->d_wf_fb_s[slot].fit(sizeof(uint32_t) * std::max<uint64_t>(q, 1)) == hipSuccess)) {
+           c->d_wf_fb_s[slot].fit(2 * sizeof(float4) * std::max<uint64_t>(q, 1)) == hipSuccess)) {
         wavefront = true;
         W.rays = c->d_wf_rays_s[slot].as<float4>();
         W.rays_b = W.rays + std::max<uint64_t>(q, 1);
@@ -1583,7 +1594,7 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
           ST.wroot = c->gv_wroot;
           ST.big_leaves = c->d_gv_big.as<uint2>();
           A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 12);
-          A.fb_list = c->d_wf_fb_s[slot].as<uint32_t>();
+          A.fb_rays = c->d_wf_fb_s[slot].as<float4>();
           A.fb_count = counter + 224;  // (zeroed with the chunk's claim counters)
           launch_grid_tree_stream(ST, S, A, stats, env_int("DRT_WAVEFRONT_WAVES", 7), F2.grid_walk, F2.grid_pairs,
                                   counter + 240, st);

@@ -897,34 +897,25 @@ __device__ __forceinline__ bool grid_box_missed(const SceneArgs& S, const RayP& 
 // The Grid cell certificate of a shadow-tree hit (trace_stream GV).  Primitive P was hit at t < range.
 // Grid::Traverse(Ray&) (grid.cpp:309-358) tests P as soon as its DDA enters any cell of P's cell range
 // (Grid::Build registers P in every cell of [min, max] of its box, grid.cpp:78-92), and the walk
-// covers the ray from its start to the grid's exit.  The ray's point at t, p = o + t d (in double), lies
-// in the grid; if it lies in a cell c of P's range, more than `margin` of a cell from each of c's faces,
-// the DDA visits c — its face crossing times are the float-rounded Init_Traverse values stepped in
-// double, off by less than 16 eps K n cells after n steps (|t_min|, |dt| and the products each carry a
-// few float roundings of values up to K grid widths, K = 1 + max_a (|min_a| + |max_a|) / width_a), and
-// the walk's start cell is off only within that distance of a face — so the walk tests P there and
-// answers occluded (or finds another occluder first).  margin = 128 eps K n_max, 8x that bound.
-// rng0 = (ix_min, iy_min, iz_min, ix_max), rng1 = (iy_max, iz_max, ., .) as floats.
+// covers the ray from its start to the grid's exit.  The ray's point at t, p = o + t d, lies in the
+// grid; if it lies in a cell c of P's range, more than S.gmargin of a cell from each of c's faces, the
+// DDA visits c — its face crossing times are the float-rounded Init_Traverse values stepped in double,
+// off by less than 16 eps K n cells after n steps (|t_min|, |dt| and the products each carry a few float
+// roundings of values up to K grid widths, K = 1 + max_a (|min_a| + |max_a|) / width_a), and the walk's
+// start cell is off only within that distance of a face — so the walk tests P there and answers
+// occluded (or finds another occluder first).  The cell coordinate u = (o + t d - min) * n / width is
+// computed here in float, within 5 eps K n cells of the real one; S.gmargin = 128 eps K n_max (scene_args)
+// is 6x the two bounds together.  rng0 = (ix_min, iy_min, iz_min, ix_max), rng1 = (iy_max, iz_max, ., .).
 __device__ __forceinline__ bool grid_certificate(const SceneArgs& S, const RayP& r, float t, const float4& rng0,
                                                  const float4& rng1) {
-  const int nm = max(S.gdim[0], max(S.gdim[1], S.gdim[2]));
-  double K = 1.0;
-#pragma unroll
-  for (int a = 0; a < 3; a++)
-    K = fmax(K, 1.0 + (fabs((double)S.gmin[a]) + fabs((double)S.gmax[a])) / ((double)S.gmax[a] - (double)S.gmin[a]));
-  const double margin = 128.0 * 0x1p-23 * K * (double)nm;
-  const double td = (double)t;
-  bool ok = margin < 0.25;  // (false for NaN: a degenerate grid leaves every query to the walk)
-  const float lo[3] = {rng0.x, rng0.y, rng0.z}, hi[3] = {rng0.w, rng1.x, rng1.y};
-  const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
-#pragma unroll
-  for (int a = 0; a < 3; a++) {
-    const double p = (double)o[a] + td * (double)d[a];
-    const double u = (p - (double)S.gmin[a]) * (double)S.gdim[a] / ((double)S.gmax[a] - (double)S.gmin[a]);
-    const double c = floor(u), f = u - c;
-    ok = ok && f > margin && f < 1.0 - margin && c >= (double)lo[a] && c <= (double)hi[a];
-  }
-  return ok;  // (false for NaN)
+  const float m = S.gmargin;
+  const float ux = (r.o.x + t * r.d.x - S.gmin[0]) * S.gscale[0];
+  const float uy = (r.o.y + t * r.d.y - S.gmin[1]) * S.gscale[1];
+  const float uz = (r.o.z + t * r.d.z - S.gmin[2]) * S.gscale[2];
+  const float cx = floorf(ux), cy = floorf(uy), cz = floorf(uz);
+  const float fx = ux - cx, fy = uy - cy, fz = uz - cz;
+  return fx > m && fx < 1.0f - m && fy > m && fy < 1.0f - m && fz > m && fz < 1.0f - m &&  // (false for NaN)
+         cx >= rng0.x && cx <= rng0.w && cy >= rng0.y && cy <= rng1.x && cz >= rng0.z && cz <= rng1.y;
 }
 
 // Grid::Init_Traverse (grid.cpp:160-245) for the lane's query: grid-box entry, first cell and
@@ -2684,7 +2675,7 @@ struct TLane {
 // GV (round 6): the Grid scene's wavefront shadow queries on its shadow tree (node_step GV; S carries the
 // Grid and, in its BVH fields, the tree): a ray that misses the grid box is occluded (grid.cpp:323), a
 // certified hit is occluded, no hit is not, and the rest (no certificate, or a ray the tree does not
-// take) go to A.fb_list for grid_fallback, which walks the Grid.
+// take) go to A.fb_rays for grid_stream, which walks the Grid.
 template <bool TRI_ONLY, int KIND, int WAVES, bool STATS, bool GV = false>
 __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, TraceArgs A) {
   constexpr int CAP = lds_cap(WAVES);
@@ -2767,7 +2758,6 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
           L.cur = S.root_desc;
           const bool fin = ray_finite(L.q);
           if constexpr (GV) {
-            L.best_prim = (uint32_t)at;  // (the query's position, for grid_fallback)
             const bool wok = fin && wide_ray_ok(L.q);
             const bool missed = grid_box_missed(S, L.q);
             L.fl = LF_SHADOW | LF_FINITE | (missed ? LF_HIT : (wok ? (LF_TRAV | LF_WIDE) : LF_GVFB));
@@ -2812,7 +2802,9 @@ __global__ void __launch_bounds__(kPBlock, WAVES) trace_stream(SceneArgs S, Trac
     }
     if (L.item != kNoItem && !(L.fl & LF_TRAV)) {  // query done: write its result
       if (GV && (L.fl & LF_GVFB)) {  // the Grid walk answers it (grid_fallback)
-        A.fb_list[atomicAdd(A.fb_count, 1u)] = L.best_prim;
+        const uint32_t k = atomicAdd(A.fb_count, 1u);
+        A.fb_rays[2 * (size_t)k] = make_float4(L.q.o.x, L.q.o.y, L.q.o.z, L.thr);
+        A.fb_rays[2 * (size_t)k + 1] = make_float4(L.q.d.x, L.q.d.y, L.q.d.z, __uint_as_float(L.item));
         if (STATS) C.v[ST_W_GRIDFB]++;
       } else if (KIND == 2) {
         wf_st(&A.occ_out[L.item], (uint8_t)((L.fl & LF_HIT) ? 1 : 0));
@@ -2855,9 +2847,9 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t chunk_next = 0, chunk_end = 0, chunk_base = 0, chunk_cnt = 0;  // wave-uniform (as trace_stream)
   bool exhausted = false;
-  // A.fb_list (round 6): the queries the Grid scene's shadow tree left undecided (trace_stream GV), a
-  // dense list of *A.fb_count positions in the compact query array, claimed 256 at a time
-  const uint32_t fb_n = A.fb_list ? __builtin_amdgcn_readfirstlane(*(volatile const uint32_t*)A.fb_count) : A.n;
+  // A.fb_rays (round 6): the queries the Grid scene's shadow tree left undecided (trace_stream GV), a
+  // dense list of *A.fb_count queries, claimed 256 at a time
+  const uint32_t fb_n = A.fb_rays ? __builtin_amdgcn_readfirstlane(*(volatile const uint32_t*)A.fb_count) : A.n;
   uint32_t part = A.parts > 1 ? (__builtin_amdgcn_s_getreg(GETREG_IMMED(3, 0, 20)) & 7u) % (uint32_t)A.parts : 0u;
   uint32_t parts_done = 0;
   while (true) {
@@ -2871,7 +2863,7 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
         base = __shfl(base, 0, 64) + pbeg;
         chunk_base = base;
         chunk_next = chunk_end = 0;
-        if (A.fb_list) {  // the shadow tree's undecided queries: a dense list of positions
+        if (A.fb_rays) {  // the shadow tree's undecided queries: a dense list
           chunk_end = base < pend ? min(base + kTraceChunk, pend) - base : 0u;
         } else if (base < pend) {  // the chunk's four group counts (one row of the query array)
           const uint32_t row = base / A.band, o0 = base - row * A.band, bl = row / (uint32_t)A.pairs;
@@ -2890,9 +2882,9 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
           const uint32_t p1 = chunk_cnt & 0xffu, p2 = p1 + ((chunk_cnt >> 8) & 0xffu), p3 = p2 + ((chunk_cnt >> 16) & 0xffu);
           const uint32_t j = (it >= p1 ? 1u : 0u) + (it >= p2 ? 1u : 0u) + (it >= p3 ? 1u : 0u);
           const uint32_t pre = j == 0u ? 0u : (j == 1u ? p1 : (j == 2u ? p2 : p3));
-          const size_t at = A.fb_list ? (size_t)A.fb_list[chunk_base + it] : (size_t)(chunk_base + 64u * j + (it - pre));
-          const float4 a = wf_ld(&A.rays[at]);
-          const float4 b = wf_ld(&A.rays_b[at]);
+          const size_t at = (size_t)(chunk_base + 64u * j + (it - pre)), fb = 2 * (size_t)(chunk_base + it);
+          const float4 a = A.fb_rays ? A.fb_rays[fb] : wf_ld(&A.rays[at]);
+          const float4 b = A.fb_rays ? A.fb_rays[fb + 1] : wf_ld(&A.rays_b[at]);
           L.item = __float_as_uint(b.w);
           L.fl = 0u;
           // a shadow ray that misses the grid box counts as shadowed (grid.cpp:323-324, Q8): start_query
@@ -2925,14 +2917,13 @@ __global__ void __launch_bounds__(256, WAVES) grid_stream(SceneArgs S, TraceArgs
 
 // The Grid scene's shadow queries that the shadow tree left undecided (trace_stream GV): each on
 // Grid::Traverse(Ray&) (grid.cpp:309-358, grid_traverse), one per thread over the list trace_stream
-// appended (A.fb_list: the queries' positions in the compact array, *A.fb_count of them).
+// appended (A.fb_rays, *A.fb_count of them).
 template <bool TRI_ONLY>
 __global__ void __launch_bounds__(256) grid_fallback(SceneArgs S, TraceArgs A) {
   Counters C;
   const uint32_t n = *A.fb_count;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-    const uint32_t at = A.fb_list[i];
-    const float4 a = A.rays[at], b = A.rays_b[at];
+    const float4 a = A.fb_rays[2 * (size_t)i], b = A.fb_rays[2 * (size_t)i + 1];
     const RayP r = make_ray(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
     float t;
     uint32_t prim;
@@ -3428,7 +3419,7 @@ static void launch_grid_stream_w(const SceneArgs& S, const TraceArgs& A, int wal
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)grid));
   hipLaunchKernelGGL((grid_stream<T, W, ST>), dim3(blocks), dim3(256), lds, st, S, A, walk, pairs);
 }
-// (A.fb_list / fb_count; fb_counter: a zeroed claim counter for the second launch)
+// (A.fb_rays / fb_count; fb_counter: a zeroed claim counter for the second launch)
 void launch_grid_tree_stream(const SceneArgs& ST_, const SceneArgs& SG, const TraceArgs& A, bool stats, int waves,
                              int walk, int pairs, unsigned int* fb_counter, hipStream_t st) {
   if (stats) launch_stream_w<true, 2, 7, true, true>(ST_, A, st);

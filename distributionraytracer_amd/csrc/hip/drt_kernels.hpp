@@ -107,6 +107,9 @@ struct SceneArgs {
   // Grid
   int gdim[3];
   float gmin[3], gmax[3];
+  // the Grid shadow tree's cell certificate (grid_certificate): cells per unit length per axis, n / width,
+  // and the margin to a cell face, in cells
+  float gscale[3], gmargin;
   const uint32_t* cell_start;
   const uint32_t* cell_objs;
   // macro-cell occupancy bitmap: bit (x>>shift) + mx*((y>>shift) + my*(z>>shift)) set if any
@@ -251,7 +254,7 @@ struct TraceArgs {
   uint32_t part_len;
   // the Grid scene's shadow tree (trace_stream GV): queries it leaves to the Grid walk, by their position
   // in the query array, and their count (grid_fallback)
-  uint32_t* fb_list;
+  float4* fb_rays;  // two per query: (o, range), (d, its slot)
   unsigned int* fb_count;
 };
 
