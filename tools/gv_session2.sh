@@ -13,7 +13,7 @@ rc=$?; echo "stats rc=$rc $(cat $OUT/gv_stats.json)"
 [ $rc -eq 0 ] || { tail -5 $OUT/gv_stats.err; exit $rc; }
 : > $OUT/gv_ab.jsonl
 for rep in 1 2; do
-  for v in "DRT_GRID_SHADOW_TREE=1" "DRT_GRID_TREE_FALLBACK_THREADS=1" "DRT_GRID_SHADOW_TREE=0"; do
+  for v in ${GV_VARIANTS:-"DRT_GRID_SHADOW_TREE=1" "DRT_GRID_TREE_WIDEN_LOG2=-17" "DRT_GRID_SHADOW_TREE=0"}; do
     env $v timeout -k 10 300 python bench.py --accel grid --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline \
       > $OUT/gv_ab.json 2> $OUT/gv_ab.err
     rc=$?
