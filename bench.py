@@ -481,7 +481,11 @@ def main():
                 # the path kernel's MODE_QSTREAM over the marker layout (DRT_GRID_STREAM=0 / DRT_WAVEFRONT_COMPACT=0)
                 compact = os.environ.get("DRT_WAVEFRONT_COMPACT", "1") != "0" and (
                     args.accel == "bvh" or os.environ.get("DRT_GRID_STREAM", "1") != "0")
+                # (round 6: a triangle scene's Grid frame answers them on its shadow tree, trace_stream GV, and
+                # the undecided ones on grid_stream; DRT_GRID_SHADOW_TREE=0 keeps grid_stream for all)
+                gv = compact and args.accel == "grid" and os.environ.get("DRT_GRID_SHADOW_TREE", "1") != "0"
                 stream_name = ("trace_stream<shadow>" if args.accel == "bvh" else
+                               "trace_stream<Grid shadow tree> + grid_stream<undecided>" if gv else
                                "grid_stream" if compact else "path_persistent<GRID> query stream")
                 row["kernels"] = (f"wf_gen + {stream_name} + wf_combine" if wavefront else
                                   f"path_persistent<{args.accel.upper()}> replay")
@@ -571,7 +575,9 @@ def main():
                      "two_level_model": model,
                      "kernel": f"path_persistent<{args.accel.upper()}>" + (
                          (" closest chain + wavefront replay (wf_gen, trace_stream, wf_combine)" if args.accel == "bvh" else
-                          " closest chain + wavefront replay (wf_gen, grid_stream, wf_combine)") if wavefront else
+                          (" closest chain + wavefront replay (wf_gen, trace_stream on the Grid's shadow tree + grid_stream, "
+                           "wf_combine)" if os.environ.get("DRT_GRID_SHADOW_TREE", "1") != "0" else
+                           " closest chain + wavefront replay (wf_gen, grid_stream, wf_combine)")) if wavefront else
                          " closest chain + replay" if passes == 2 else ""),
                      "bytes_per_launch": int(bytes_launch),
                      "kernel_ms": round(kernel_ms, 3), "kernel_ms_serial": round(serial_ms, 3),

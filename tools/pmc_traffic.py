@@ -56,7 +56,8 @@ def last_frame(counters, sub=None):
                 cur[q] = [k]
                 frames.append(cur[q])
         elif ("wf_gen_kernel" in name or "wf_combine" in name or
-              (("trace_stream<" in name or "grid_stream<" in name) and a and a[-1] == "false")) and cur.get(q) is not None:
+              (("trace_stream<" in name and len(a) > 3 and a[3] == "false") or (
+               "grid_stream<" in name and len(a) > 2 and a[2] == "false"))) and cur.get(q) is not None:
             cur[q].append(k)
     return frames[-1] if frames else []
 

@@ -56,7 +56,8 @@ def main():
                 cur[stream] = [(s0, e0, k)]
                 frames.append(cur[stream])
         elif ("wf_gen_kernel" in k or "wf_combine" in k or
-              (("trace_stream<" in k or "grid_stream<" in k) and targs[-1].strip() == "false")) and cur.get(stream) is not None:
+              (("trace_stream<" in k and targs[3].strip() == "false") or (
+               "grid_stream<" in k and targs[2].strip() == "false"))) and cur.get(stream) is not None:
             cur[stream].append((s0, e0, k))
     names = sorted({k for fr in frames for _, _, k in fr})
     P = max((len(fr) for fr in frames), default=1)
