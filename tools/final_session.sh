@@ -6,7 +6,8 @@
 #      bench line and a rocprofv3 --kernel-trace --stats run of the same command (tools/gpu_check.sh, no tests)
 #   Z: Y without the PMC passes, plus the 2-rank multi-rank rehearsal (tools/multirank_check.sh)
 #   G: the Grid PMC record after grid_stream + Z's bench evidence; H: tests, smoke, multi-rank, shard scaling
-#   usage: bash tools/final_session.sh X|Y|Z|G|H
+#   F: the Grid PMC record after the Grid shadow tree, tests, smoke, configs, bench + rocprof union
+#   usage: bash tools/final_session.sh X|Y|Z|G|H|F
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
@@ -49,6 +50,13 @@ case "${1:-X}" in
         python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || exit $?
     python tools/rocprof_union.py $OUT/prof --steps 20 --warmup 2 --bench-json $OUT/prof_bench.json > $OUT/rocprof_union.json || exit $?
     cat $OUT/rocprof_union.json
+    ;;
+  F)  # after the Grid scene's shadow tree: the Grid PMC record (its pass 2 now trace_stream GV + grid_stream),
+      # the parity tests, smoke, every config, the bench line and its rocprof union
+    cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
+    PMC_DB=$OUT/pmc_traffic.json bash tools/session.sh "pmc:grid" || exit $?
+    cp $OUT/pmc_traffic.json profiles/pmc_traffic.json
+    CFG_STEPS=10 bash tools/session.sh tests smoke configs "bench:--steps 20 --warmup 2" "prof:--steps 20 --warmup 2" || exit $?
     ;;
   H)  # the parity tests, smoke, the multi-rank rehearsal and the shard scaling at the head
     bash tools/session.sh tests smoke mr:2 "shards:--steps 40 --pipe 2" || exit $?
