@@ -325,3 +325,28 @@ def test_grid_vs_bvh_tool_covers_the_shipped_grid_scenes(tmp_path):
     for n in sorted(grid_default):
         s = drt.Scene.load_p3f(shipped.write(tmp_path, n), skybox_faces=shipped.skybox_faces(n))
         assert s.info().accel == 1, n
+
+
+@pytest.mark.parametrize("case", ["mixed", "tris2k"])
+def test_reference_grid_lists_each_object_in_a_whole_box_of_cells(case):
+    """The premise of the Grid shadow tree's cell certificate (round 6, grid_certificate): Grid::Build lists
+    an object in EVERY cell of the box [min, max] of its cell coordinates (grid.cpp:78-92), so the min / max
+    over the cells that list it (drt_upload_grid's per-object ranges) is that box, and a cell inside it lists
+    the object.  Checked on the reference-run grids of the golden fixtures."""
+    g = np.load(GOLD / f"ref_{case}.npz")
+    nx, ny, nz = (int(d) for d in g["grid_dims"])
+    cs, co = g["grid_cell_start"], g["grid_cell_objs"]
+    cell = np.repeat(np.arange(nx * ny * nz), np.diff(cs))
+    x, y, z = cell % nx, (cell // nx) % ny, cell // (nx * ny)
+    n_obj = int(co.max()) + 1
+    lo = np.full((n_obj, 3), np.iinfo(np.int64).max)
+    hi = np.full((n_obj, 3), -1)
+    for a, v in enumerate((x, y, z)):
+        np.minimum.at(lo[:, a], co, v)
+        np.maximum.at(hi[:, a], co, v)
+    count = np.bincount(co, minlength=n_obj)
+    listed = count > 0
+    assert listed.all()
+    np.testing.assert_array_equal(count, np.prod(hi - lo + 1, axis=1))
+    # and no object is listed twice in one cell
+    assert len(np.unique(cell * n_obj + co)) == len(co)
