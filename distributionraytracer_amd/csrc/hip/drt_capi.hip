@@ -1596,7 +1596,9 @@ static int run_frame(drt_ctx* c, const drt_frame_params* p, float* d_out, bool f
           ST.wleaf = c->d_gv_range.as<float4>();
           ST.wroot = c->gv_wroot;
           ST.big_leaves = c->d_gv_big.as<uint2>();
-          A.refill_min = env_int("DRT_WAVEFRONT_REFILL_MIN", 12);
+          // refill at 16 idle lanes: 2 162-2 165 against 2 148 Mrays/s at the BVH stream's 12 (8: 2 098; 6 waves
+          // instead of 7: 2 138-2 145; profiles/r06_ab_grid_shadow_tree_knobs.jsonl)
+          A.refill_min = env_int("DRT_GRID_TREE_REFILL_MIN", 16);
           A.fb_rays = c->d_wf_fb_s[slot].as<float4>();
           A.fb_count = counter + 224;  // (zeroed with the chunk's claim counters)
           launch_grid_tree_stream(ST, S, A, stats, env_int("DRT_WAVEFRONT_WAVES", 7), F2.grid_walk, F2.grid_pairs,
